@@ -1,0 +1,232 @@
+#!/usr/bin/env python3
+"""Benchmark: Mray/s (samples x bounces) on the Cornell box at 1024^2 @ 1000 spp (BASELINE.json configs[1]).
+
+One step = one full progressive render of the workload on the rank's share of the image:
+Reset() + spp x Update() (executed as kernel launches of --launch-frames frames each) + the RCCL
+gather of every rank's row bands to rank 0 and the de-interleave there. Rays = closest-hit
+queries issued by RayColor (one per bounce level with depth > 0), counted by the
+kernel. Inputs (scene program) are resident in HBM before timing starts.
+
+  python bench.py [--gpus N --steps K --warmup W]      (N > 1: launched by torch.distributed.run)
+
+Rank 0 prints one JSON line (contract in the task statement) with a `roofline` object for the
+render kernel (algorithmic bytes per launch / HIP-event launch time vs 8 TB/s HBM) and a
+`cpu_baseline` object (the oracle restatement timed on this host's cores on a bounded sample).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402  (import before raytrace2_amd: one HIP runtime per process)
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP32_VALU_PEAK_TFLOPS = 157.3
+# Record sizes of the flattened scene program (rt2_layout.h) in bytes
+REC_BYTES = {"bvh_tests": 32, "quad_tests": 80, "sphere_tests": 32, "xform_visits": 128, "medium_tests": 16,
+             "list_visits": 16}
+FLOPS = {"bvh_tests": 18, "quad_tests": 45, "sphere_tests": 30, "xform_visits": 45, "medium_tests": 20}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scene", default="cornell_box_original.json")
+    ap.add_argument("--width", type=int, default=1024)
+    ap.add_argument("--height", type=int, default=1024)
+    ap.add_argument("--spp", type=int, default=1000)
+    ap.add_argument("--max-depth", type=int, default=50)
+    ap.add_argument("--seed", type=int, default=0x5EED2024)
+    ap.add_argument("--band-h", type=int, default=16)
+    ap.add_argument("--launch-frames", type=int, default=0, help="frames per kernel launch (0 = all)")
+    ap.add_argument("--cpu-frames", type=int, default=4, help="oracle sample: frames at full resolution")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--stats-frames", type=int, default=8)
+    ap.add_argument("--out-image", default="")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+
+    import raytrace2_amd as R
+
+    scene_file = os.path.join(ROOT, "scenes", a.scene)
+    t0 = time.perf_counter()
+    sc = R.Scene(scene_file, a.seed)
+    tr = R.RayTracer(sc, local_rank)
+    stream = torch.cuda.current_stream(dev)
+    tr.set_stream(stream.cuda_stream)
+    tr.set_seed(a.seed)
+    tr.max_depth = a.max_depth
+    tr.SetSamplesPerPixel(a.spp)
+    tr.OnResize((a.width, a.height))
+    tr.set_partition(a.band_h, rank, world)
+    if a.launch_frames:
+        tr.set_launch_frames(a.launch_frames)
+    tr.synchronize()
+    setup_s = time.perf_counter() - t0
+    rows = tr.local_rows()
+    max_rows = -(-a.height // (a.band_h * world)) * a.band_h  # upper bound of rows per rank
+    local = torch.zeros((max_rows, a.width, 3), dtype=torch.float32, device=dev)
+    gathered = [torch.zeros_like(local) for _ in range(world)] if rank == 0 else None
+    image = torch.zeros((a.height, a.width, 3), dtype=torch.float32, device=dev) if rank == 0 else None
+    row_index = None
+    if rank == 0:
+        idx = []
+        for r in range(world):
+            ys = R.local_rows(a.height, a.band_h, r, world)
+            idx.append(torch.tensor(ys, dtype=torch.long, device=dev))
+        row_index = idx
+
+    def step():
+        tr.Reset()
+        tr.Render(a.spp)
+        tr.copy_accum_to(local.data_ptr(), stream.cuda_stream)
+        if world > 1:
+            dist.gather(local, gathered if rank == 0 else None, dst=0)
+            if rank == 0:
+                for r in range(world):
+                    n = row_index[r].numel()
+                    image.index_copy_(0, row_index[r], gathered[r][:n])
+        else:
+            image[:rows].copy_(local[:rows])
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    tr.reset_stats()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t_start = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(a.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    st = tr.stats()
+    stream_ms = ev0.elapsed_time(ev1)
+    rays_local = st["rays"]
+    kernel_ms = st["kernel_ms"]
+    launches = max(1, st["launches"])
+    if world > 1:
+        t = torch.tensor([elapsed, float(rays_local)], dtype=torch.float64, device=dev)
+        tmax = t.clone()
+        dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+        elapsed = float(tmax[0])
+        rays_total = float(t[1])
+    else:
+        rays_total = float(rays_local)
+
+    if rank == 0 and a.out_image:
+        img = image.cpu().numpy() / np.float32(a.spp)
+        R.WriteImage(img, a.width, a.height, a.out_image)
+
+    # ---- algorithmic bytes per ray from a stats pass (same seed, same kernel family) ----
+    roofline = None
+    if rank == 0:
+        tr.enable_stats(True)
+        tr.Reset()
+        tr.reset_stats()
+        tr.Render(a.stats_frames)
+        s2 = tr.stats()
+        tr.enable_stats(False)
+        per_ray = {k: s2[k] / max(1, s2["rays"]) for k in REC_BYTES}
+        b_ray = sum(REC_BYTES[k] * per_ray[k] for k in REC_BYTES)
+        f_ray = sum(FLOPS.get(k, 0) * per_ray[k] for k in REC_BYTES)
+        rays_per_launch = rays_local / launches
+        pixels_local = rows * a.width
+        frame_bytes = pixels_local * (12 + 12 + 4)  # accum read + write, RGBA8 write per launch
+        bytes_per_launch = rays_per_launch * b_ray + frame_bytes
+        avg_launch_s = kernel_ms / 1e3 / launches
+        achieved = bytes_per_launch / avg_launch_s / 1e9
+        roofline = {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": None,
+            "kernel": "rt2::dev::render_kernel<false>",
+            "avg_launch_ms": round(kernel_ms / launches, 3),
+            "bytes_per_ray": round(b_ray, 1),
+            "records_per_ray": {k: round(v, 3) for k, v in per_ray.items()},
+            "valu_frac": round(rays_per_launch * f_ray / avg_launch_s / 1e12 / FP32_VALU_PEAK_TFLOPS, 4),
+        }
+
+    cpu = None
+    if rank == 0 and not a.no_cpu and world == 1:
+        from oracle.oracle import OracleScene
+        try:
+            cores = min(16, len(os.sched_getaffinity(0)))
+        except AttributeError:
+            cores = min(16, os.cpu_count() or 1)
+        o = OracleScene(scene_file, a.seed)
+        tc = time.perf_counter()
+        _, _, cnt = o.render(a.width, a.height, a.spp, a.cpu_frames, max_depth=a.max_depth, threads=cores,
+                             forward=False)
+        dt = time.perf_counter() - tc
+        cpu = {"value": round(cnt["rays"] / dt / 1e6, 3), "unit": "Mray/s", "cores": cores, "kind": "port",
+               "sample": f"{a.scene} {a.width}x{a.height}, frames 0..{a.cpu_frames - 1} of the spp={a.spp} "
+                         f"stratification, oracle restatement (recursive RayColor), {cnt['rays']} rays in "
+                         f"{dt:.2f} s"}
+
+    if rank == 0:
+        value = rays_total / elapsed / 1e6
+        out = {
+            "metric": "Mray/s (samples x bounces) Cornell Box 1024^2 @ 1000 spp",
+            "value": round(value, 2),
+            "unit": "Mray/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(elapsed * 1e3 / a.steps, 2),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: committed scene JSON (scenes/), Philox4x32-10 sample streams seeded "
+                    f"{a.seed:#x}",
+            "config": {"workload": f"{a.scene} {a.width}x{a.height} @ {a.spp} spp, max_depth {a.max_depth}",
+                       "parallelism": f"row-bands h={a.band_h} x {world} GPU(s), RCCL gather to rank 0",
+                       "launch_frames": a.launch_frames or a.spp},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "detail": {"rays": int(rays_total), "stream_ms": round(stream_ms, 2),
+                       "kernel_ms_per_step": round(kernel_ms / a.steps, 2), "launches": launches,
+                       "setup_s": round(setup_s, 3),
+                       "rays_per_sample": round(rays_total / (a.steps * a.spp * a.width * a.height), 4)},
+        }
+        if cpu:
+            out["detail"]["gpu_over_cpu"] = round(value / cpu["value"], 1)
+        print(json.dumps(out), flush=True)
+    tr.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

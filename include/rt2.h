@@ -1,0 +1,141 @@
+/* rt2.h — C ABI of the MI355X (gfx950) replacement for the reference renderer's hot path.
+ *
+ * Drop-in boundary for tonadr1022/Raytrace2 `raytrace2::cpu::RayTracer` (src/cpu_raytrace/
+ * RayTracer.hpp:15-42) and the host surface that stays around it: `serialize::SceneLoader`,
+ * `LoadCamera`, `WriteCamera`, `LoadAppSettings` (src/Serialize.hpp:21-35) and
+ * `util::WriteImage` (src/Util.hpp:11-12). Plain pointers and sizes only; no HIP or torch types in
+ * the signatures (streams are passed as void*). Every function returns RT2_OK (0) or a negative
+ * status and never throws; rt2_last_error() has the message (thread-local).
+ *
+ * Pixel layout: row-major, row 0 = bottom image row (RayTracer.cpp:97-102). With a row-band
+ * partition (rt2_tracer_set_partition) a tracer owns the "local rows" y with
+ * (y / band_h) % world == rank, stored compactly in increasing y.
+ */
+#ifndef RT2_H_
+#define RT2_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT2_API __attribute__((visibility("default")))
+
+enum {
+  RT2_OK = 0,
+  RT2_ERR_INVALID = -1, /* bad argument or call order */
+  RT2_ERR_IO = -2,      /* file missing / unreadable / unwritable */
+  RT2_ERR_SCENE = -3,   /* scene schema or compile error */
+  RT2_ERR_HIP = -4,     /* HIP runtime error (no device, out of memory, launch failure) */
+};
+
+typedef struct rt2_scene rt2_scene;
+typedef struct rt2_tracer rt2_tracer;
+
+RT2_API const char* rt2_last_error(void);
+RT2_API const char* rt2_version(void);
+
+/* ---- SceneLoader::LoadScene (Serialize.cpp:199-360) + App.cpp:126 (top-level BVHNode) ----
+ * Accepts the v2 schema and the legacy {"primitives":{"spheres":[...]}} schema (documented
+ * adapter: each sphere is a top-level node; a missing camera means "cam1"). Camera names resolve
+ * to <scene dir>/<name>.json. `seed` keys the Perlin-table random streams (the reference draws them
+ * from its unseeded RNG at load, PerlinNoiseGen.cpp:41-50). */
+RT2_API int rt2_scene_load(const char* path, uint64_t seed, rt2_scene** out);
+RT2_API void rt2_scene_free(rt2_scene* scene);
+
+typedef struct {
+  int dims_x, dims_y; /* Scene::dims (camera width / aspect), 0 when absent */
+  int n_materials, n_textures, n_primitives, n_top_nodes;
+  float background[3];
+  int legacy_schema;
+  int bvh_nodes, quads, spheres, lists, xforms, media; /* flattened records */
+  int max_stack, bvh_depth;
+  uint64_t node_bytes;
+} rt2_scene_info;
+RT2_API int rt2_scene_get_info(const rt2_scene* scene, rt2_scene_info* out);
+/* Material table, 8 floats per material: type, albedo.xyz, fuzz, refraction_index, tex_idx, 0.
+ * type: 0 metal, 1 lambertian, 2 dielectric, 3 texture, 4 diffuse_light, 5 isotropic
+ * (variant order of Fwd.hpp:13-14). Returns the material count. */
+RT2_API int rt2_scene_materials(const rt2_scene* scene, float* out, int cap);
+/* Texture table, 8 floats: type (0 solid, 1 checker, 2 noise), albedo.xyz, inv_scale|scale,
+ * even, odd, noise_type. Returns the texture count. */
+RT2_API int rt2_scene_textures(const rt2_scene* scene, float* out, int cap);
+/* Perlin tables of noise texture `tex`: vec = point_count*3 floats, perm = 3*point_count ints
+ * (perm_x, perm_y, perm_z). Returns point_count. */
+RT2_API int rt2_scene_perlin(const rt2_scene* scene, int tex, float* vec, int* perm);
+
+/* ---- Camera (Camera.hpp:10-137) ---- */
+typedef struct {
+  float center[3], look_at[3], view_up[3];
+  float vfov, defocus_angle, focus_distance;
+} rt2_camera_desc;
+RT2_API int rt2_scene_get_camera(const rt2_scene* scene, rt2_camera_desc* out);
+RT2_API int rt2_scene_set_camera(rt2_scene* scene, const rt2_camera_desc* cam);
+/* Camera::Update for (w, h, spp): out[21] = pixel00(3) du(3) dv(3) center(3) defocus_u(3)
+ * defocus_v(3) defocus_angle recip_sqrt_spp sqrt_spp */
+RT2_API int rt2_camera_params(const rt2_scene* scene, int w, int h, int spp, float* out);
+RT2_API int rt2_camera_load(const char* path, rt2_camera_desc* out);         /* LoadCamera */
+RT2_API int rt2_camera_write(const rt2_camera_desc* cam, const char* path);  /* WriteCamera */
+
+/* ---- LoadAppSettings (Serialize.cpp:56-65) ---- */
+typedef struct {
+  int render_once, save_after_render_once;
+  int64_t num_samples, max_depth;
+  int render_window;
+} rt2_app_settings;
+RT2_API int rt2_settings_load(const char* path, rt2_app_settings* out);
+
+/* ---- RayTracer (RayTracer.hpp:15-42) on one GPU ----
+ * create:   compiles the scene program and uploads it to `device` (the scene may be freed after).
+ * on_resize:OnResize(dims) (RayTracer.cpp:87-104): sets camera dims, reallocates, Reset().
+ * update:   Update(scene) (RayTracer.cpp:55-70): one frame, stratum (f % sq, f / sq % sq).
+ * render:   n consecutive Update() calls, executed as ceil(n / launch_frames) kernel launches.
+ * Frames are enqueued on the tracer's stream; readbacks synchronise it. */
+RT2_API int rt2_tracer_create(const rt2_scene* scene, int device, rt2_tracer** out);
+RT2_API void rt2_tracer_destroy(rt2_tracer* tr);
+RT2_API int rt2_tracer_set_stream(rt2_tracer* tr, void* hip_stream); /* NULL = own stream */
+RT2_API int rt2_tracer_set_max_depth(rt2_tracer* tr, int max_depth); /* RayTracer::max_depth */
+RT2_API int rt2_tracer_set_samples_per_pixel(rt2_tracer* tr, int spp); /* App.cpp:129 */
+RT2_API int rt2_tracer_set_seed(rt2_tracer* tr, uint64_t seed);
+RT2_API int rt2_tracer_set_partition(rt2_tracer* tr, int band_h, int rank, int world);
+RT2_API int rt2_tracer_set_launch_frames(rt2_tracer* tr, int frames_per_launch); /* 0 = all */
+RT2_API int rt2_tracer_on_resize(rt2_tracer* tr, int width, int height);
+RT2_API int rt2_tracer_reset(rt2_tracer* tr);
+RT2_API int rt2_tracer_update(rt2_tracer* tr);
+RT2_API int rt2_tracer_render(rt2_tracer* tr, int n_frames);
+RT2_API int rt2_tracer_synchronize(rt2_tracer* tr);
+RT2_API int64_t rt2_tracer_frame_idx(const rt2_tracer* tr); /* FrameIdx */
+RT2_API int rt2_tracer_dims(const rt2_tracer* tr, int* width, int* height); /* Dims */
+RT2_API int rt2_tracer_local_rows(const rt2_tracer* tr);
+/* NonConvertedPixels (RayTracer.cpp:105-112): accum / frame_idx, float3 per local pixel */
+RT2_API int rt2_tracer_non_converted_pixels(rt2_tracer* tr, float* out);
+RT2_API int rt2_tracer_accumulation(rt2_tracer* tr, float* out); /* raw float3 sums */
+RT2_API int rt2_tracer_pixels(rt2_tracer* tr, uint8_t* out_rgba); /* Pixels(): RGBA8 */
+/* Device-to-device copy of the local accumulation (float3 per local pixel) into `dst_device`,
+ * ordered on `hip_stream` (NULL = tracer stream) — used for the multi-GPU gather. */
+RT2_API int rt2_tracer_copy_accum_device(rt2_tracer* tr, void* dst_device, void* hip_stream);
+RT2_API int rt2_tracer_enable_ray_counts(rt2_tracer* tr, int on);
+RT2_API int rt2_tracer_ray_counts(rt2_tracer* tr, uint32_t* out); /* rays per local pixel */
+RT2_API int rt2_tracer_enable_stats(rt2_tracer* tr, int on);      /* per-record test counters */
+
+typedef struct {
+  uint64_t rays;      /* closest-hit queries issued by RayColor (depth > 0) */
+  uint64_t paths;     /* camera samples finished */
+  uint64_t bvh_tests, quad_tests, sphere_tests, xform_visits, medium_tests, list_visits;
+  uint64_t overflow;  /* lanes that hit the traversal-stack bound (must be 0) */
+  uint64_t launches;
+  double kernel_ms;   /* sum of per-launch HIP event durations */
+} rt2_stats;
+RT2_API int rt2_tracer_get_stats(rt2_tracer* tr, rt2_stats* out);
+RT2_API int rt2_tracer_reset_stats(rt2_tracer* tr);
+
+/* ---- util::WriteImage (Util.cpp:39-79): sqrt gamma, clamp(x*255.999), vertical flip ---- */
+RT2_API int rt2_write_image(const float* pixels, int width, int height, const char* path, int png);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RT2_H_ */

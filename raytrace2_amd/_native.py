@@ -1,0 +1,127 @@
+"""ctypes binding of include/rt2.h (lib/librt2.so). No fallback: if the library is missing or fails
+to load, importing raytrace2_amd raises."""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "librt2.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "rt2.h")
+
+RT2_OK = 0
+RT2_ERR_INVALID = -1
+RT2_ERR_IO = -2
+RT2_ERR_SCENE = -3
+RT2_ERR_HIP = -4
+
+
+class Rt2Error(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"rt2 error {code}: {msg}")
+        self.code = code
+
+
+class SceneInfo(ctypes.Structure):
+    _fields_ = [("dims_x", ctypes.c_int), ("dims_y", ctypes.c_int),
+                ("n_materials", ctypes.c_int), ("n_textures", ctypes.c_int),
+                ("n_primitives", ctypes.c_int), ("n_top_nodes", ctypes.c_int),
+                ("background", ctypes.c_float * 3), ("legacy_schema", ctypes.c_int),
+                ("bvh_nodes", ctypes.c_int), ("quads", ctypes.c_int), ("spheres", ctypes.c_int),
+                ("lists", ctypes.c_int), ("xforms", ctypes.c_int), ("media", ctypes.c_int),
+                ("max_stack", ctypes.c_int), ("bvh_depth", ctypes.c_int), ("node_bytes", ctypes.c_uint64)]
+
+
+class CameraDesc(ctypes.Structure):
+    _fields_ = [("center", ctypes.c_float * 3), ("look_at", ctypes.c_float * 3),
+                ("view_up", ctypes.c_float * 3), ("vfov", ctypes.c_float),
+                ("defocus_angle", ctypes.c_float), ("focus_distance", ctypes.c_float)]
+
+
+class AppSettings(ctypes.Structure):
+    _fields_ = [("render_once", ctypes.c_int), ("save_after_render_once", ctypes.c_int),
+                ("num_samples", ctypes.c_int64), ("max_depth", ctypes.c_int64),
+                ("render_window", ctypes.c_int)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in
+                ("rays", "paths", "bvh_tests", "quad_tests", "sphere_tests", "xform_visits",
+                 "medium_tests", "list_visits", "overflow", "launches")] + [("kernel_ms", ctypes.c_double)]
+
+    def as_dict(self):
+        return {n: (getattr(self, n) if n == "kernel_ms" else int(getattr(self, n))) for n, _ in self._fields_}
+
+
+def declared_symbols(header: str = HEADER_PATH):
+    """Every RT2_API function name declared in include/rt2.h."""
+    txt = open(header).read()
+    return re.findall(r"RT2_API\s+[\w\s\*]+?\b(rt2_\w+)\s*\(", txt)
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"raytrace2_amd: {LIB_PATH} is missing — run `python -c 'import __graft_entry__ as g; "
+                          f"g.build()'` (or make -C raytrace2_amd/csrc); there is no CPU fallback")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i32, i64, u64, f32 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, ctypes.c_float
+    fp = ctypes.POINTER(ctypes.c_float)
+    pp = ctypes.POINTER(ctypes.c_void_p)
+    sig = {
+        "rt2_last_error": (ctypes.c_char_p, []),
+        "rt2_version": (ctypes.c_char_p, []),
+        "rt2_scene_load": (i32, [ctypes.c_char_p, u64, pp]),
+        "rt2_scene_free": (None, [vp]),
+        "rt2_scene_get_info": (i32, [vp, ctypes.POINTER(SceneInfo)]),
+        "rt2_scene_materials": (i32, [vp, fp, i32]),
+        "rt2_scene_textures": (i32, [vp, fp, i32]),
+        "rt2_scene_perlin": (i32, [vp, i32, fp, ctypes.POINTER(ctypes.c_int)]),
+        "rt2_scene_get_camera": (i32, [vp, ctypes.POINTER(CameraDesc)]),
+        "rt2_scene_set_camera": (i32, [vp, ctypes.POINTER(CameraDesc)]),
+        "rt2_camera_params": (i32, [vp, i32, i32, i32, fp]),
+        "rt2_camera_load": (i32, [ctypes.c_char_p, ctypes.POINTER(CameraDesc)]),
+        "rt2_camera_write": (i32, [ctypes.POINTER(CameraDesc), ctypes.c_char_p]),
+        "rt2_settings_load": (i32, [ctypes.c_char_p, ctypes.POINTER(AppSettings)]),
+        "rt2_tracer_create": (i32, [vp, i32, pp]),
+        "rt2_tracer_destroy": (None, [vp]),
+        "rt2_tracer_set_stream": (i32, [vp, vp]),
+        "rt2_tracer_set_max_depth": (i32, [vp, i32]),
+        "rt2_tracer_set_samples_per_pixel": (i32, [vp, i32]),
+        "rt2_tracer_set_seed": (i32, [vp, u64]),
+        "rt2_tracer_set_partition": (i32, [vp, i32, i32, i32]),
+        "rt2_tracer_set_launch_frames": (i32, [vp, i32]),
+        "rt2_tracer_on_resize": (i32, [vp, i32, i32]),
+        "rt2_tracer_reset": (i32, [vp]),
+        "rt2_tracer_update": (i32, [vp]),
+        "rt2_tracer_render": (i32, [vp, i32]),
+        "rt2_tracer_synchronize": (i32, [vp]),
+        "rt2_tracer_frame_idx": (i64, [vp]),
+        "rt2_tracer_dims": (i32, [vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
+        "rt2_tracer_local_rows": (i32, [vp]),
+        "rt2_tracer_non_converted_pixels": (i32, [vp, fp]),
+        "rt2_tracer_accumulation": (i32, [vp, fp]),
+        "rt2_tracer_pixels": (i32, [vp, ctypes.POINTER(ctypes.c_uint8)]),
+        "rt2_tracer_copy_accum_device": (i32, [vp, vp, vp]),
+        "rt2_tracer_enable_ray_counts": (i32, [vp, i32]),
+        "rt2_tracer_ray_counts": (i32, [vp, ctypes.POINTER(ctypes.c_uint32)]),
+        "rt2_tracer_enable_stats": (i32, [vp, i32]),
+        "rt2_tracer_get_stats": (i32, [vp, ctypes.POINTER(Stats)]),
+        "rt2_tracer_reset_stats": (i32, [vp]),
+        "rt2_write_image": (i32, [fp, i32, i32, ctypes.c_char_p, i32]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    del f32
+    return L
+
+
+lib = _load()
+
+
+def check(rc: int):
+    if rc < 0:
+        raise Rt2Error(rc, lib.rt2_last_error().decode(errors="replace"))
+    return rc

@@ -1,0 +1,650 @@
+// capi.cpp — implementation of include/rt2.h: scene handles, the device-side RayTracer and the
+// host utilities. Device memory is owned by the tracer (hipMalloc); the caller owns host buffers.
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/rt2.h"
+#include "scene.h"
+
+namespace rt2 {
+hipError_t LaunchRender(const RenderParams& p, bool stats, int grid, hipStream_t stream);
+int RenderBlocksPerCU(bool stats);
+int RenderBlockSize();
+bool WriteImage(const float* pixels, int w, int h, const std::string& path, bool png, std::string& err);
+}  // namespace rt2
+
+using namespace rt2;
+
+struct rt2_scene {
+  Scene scene;
+  CompiledScene compiled;
+};
+
+struct rt2_tracer {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  // scene program
+  void* d_nodes = nullptr;
+  void* d_materials = nullptr;
+  void* d_textures = nullptr;
+  void* d_perlin_vec = nullptr;
+  int* d_perlin_perm = nullptr;
+  uint32_t root = kRefNone;
+  float background[3] = {0, 0, 0};
+  Camera camera;  // RayTracer::camera (a copy of the scene camera)
+  // frame buffers (local rows)
+  int width = 0, height = 0, local_rows = 0;
+  int band_h = 0, rank = 0, world = 1;
+  float* d_accum = nullptr;
+  uint8_t* d_pixels = nullptr;
+  uint32_t* d_ray_counts = nullptr;
+  bool ray_counts_on = false;
+  uint32_t* d_work = nullptr;
+  unsigned long long* d_stats = nullptr;
+  bool stats_on = false;
+  int64_t frame_idx = 0;
+  int max_depth = 50;
+  uint64_t seed = 0x5EED2024ull;
+  int launch_frames = 0;
+  int grid = 0;
+  uint64_t launches = 0;
+  double kernel_ms = 0;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;  // per-launch timing events
+  std::vector<hipEvent_t> event_pool;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int Fail(int code, const std::string& m) {
+  g_err = m;
+  return code;
+}
+int HipFail(hipError_t e, const char* what) {
+  return Fail(RT2_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+#define HIP_TRY(expr)                                  \
+  do {                                                 \
+    hipError_t _e = (expr);                            \
+    if (_e != hipSuccess) return HipFail(_e, #expr);   \
+  } while (0)
+
+int LocalRows(int h, int band_h, int rank, int world) {
+  int n = 0;
+  for (int y = 0; y < h; y++)
+    if ((y / band_h) % world == rank) n++;
+  return n;
+}
+
+void FreeFrame(rt2_tracer* t) {
+  (void)hipFree(t->d_accum);
+  (void)hipFree(t->d_pixels);
+  (void)hipFree(t->d_ray_counts);
+  t->d_accum = nullptr;
+  t->d_pixels = nullptr;
+  t->d_ray_counts = nullptr;
+}
+
+int Realloc(rt2_tracer* t) {
+  FreeFrame(t);
+  int bh = t->band_h > 0 ? t->band_h : (t->height > 0 ? t->height : 1);
+  t->local_rows = t->height > 0 ? LocalRows(t->height, bh, t->rank, t->world) : 0;
+  size_t n = (size_t)t->width * (size_t)t->local_rows;
+  if (n == 0) return RT2_OK;
+  HIP_TRY(hipMalloc(&t->d_accum, n * 3 * sizeof(float)));
+  HIP_TRY(hipMalloc(&t->d_pixels, n * 4));
+  if (t->ray_counts_on) HIP_TRY(hipMalloc(&t->d_ray_counts, n * sizeof(uint32_t)));
+  return RT2_OK;
+}
+
+int ResetFrame(rt2_tracer* t) {
+  size_t n = (size_t)t->width * (size_t)t->local_rows;
+  t->frame_idx = 0;
+  if (n == 0) return RT2_OK;
+  HIP_TRY(hipMemsetAsync(t->d_accum, 0, n * 3 * sizeof(float), t->stream));
+  HIP_TRY(hipMemsetAsync(t->d_pixels, 0, n * 4, t->stream));
+  if (t->d_ray_counts) HIP_TRY(hipMemsetAsync(t->d_ray_counts, 0, n * sizeof(uint32_t), t->stream));
+  return RT2_OK;
+}
+
+hipEvent_t TakeEvent(rt2_tracer* t) {
+  if (!t->event_pool.empty()) {
+    hipEvent_t e = t->event_pool.back();
+    t->event_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+int DrainEvents(rt2_tracer* t) {
+  for (auto& pr : t->pending) {
+    HIP_TRY(hipEventSynchronize(pr.second));
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, pr.first, pr.second));
+    t->kernel_ms += ms;
+    t->event_pool.push_back(pr.first);
+    t->event_pool.push_back(pr.second);
+  }
+  t->pending.clear();
+  return RT2_OK;
+}
+
+int Sync(rt2_tracer* t) {
+  HIP_TRY(hipSetDevice(t->device));
+  HIP_TRY(hipStreamSynchronize(t->stream));
+  return DrainEvents(t);
+}
+
+template <typename T>
+int Upload(T** dst, const void* src, size_t bytes) {
+  HIP_TRY(hipMalloc((void**)dst, bytes));
+  HIP_TRY(hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice));
+  return RT2_OK;
+}
+
+void Put3(float* d, vec3 v) {
+  d[0] = v.x;
+  d[1] = v.y;
+  d[2] = v.z;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* rt2_last_error(void) { return g_err.c_str(); }
+const char* rt2_version(void) { return "rt2-mi355x 0.1 (gfx950)"; }
+
+int rt2_scene_load(const char* path, uint64_t seed, rt2_scene** out) {
+  if (!path || !out) return Fail(RT2_ERR_INVALID, "rt2_scene_load: null argument");
+  *out = nullptr;
+  auto s = std::make_unique<rt2_scene>();
+  std::string err;
+  if (!LoadScene(path, seed, s->scene, err)) {
+    bool io = err.rfind("Failed to open", 0) == 0;
+    return Fail(io ? RT2_ERR_IO : RT2_ERR_SCENE, err);
+  }
+  if (!CompileScene(s->scene, s->compiled, err)) return Fail(RT2_ERR_SCENE, err);
+  *out = s.release();
+  return RT2_OK;
+}
+
+void rt2_scene_free(rt2_scene* s) { delete s; }
+
+int rt2_scene_get_info(const rt2_scene* s, rt2_scene_info* o) {
+  if (!s || !o) return Fail(RT2_ERR_INVALID, "rt2_scene_get_info: null argument");
+  const Scene& sc = s->scene;
+  const CompiledScene& c = s->compiled;
+  o->dims_x = sc.dims_x;
+  o->dims_y = sc.dims_y;
+  o->n_materials = (int)sc.materials.size();
+  o->n_textures = (int)sc.textures.size();
+  o->n_primitives = (int)sc.primitives.size();
+  o->n_top_nodes = (int)sc.top.size();
+  Put3(o->background, sc.background);
+  o->legacy_schema = sc.legacy_schema ? 1 : 0;
+  o->bvh_nodes = c.bvh_nodes;
+  o->quads = c.quads;
+  o->spheres = c.spheres;
+  o->lists = c.lists;
+  o->xforms = c.xforms;
+  o->media = c.media;
+  o->max_stack = c.max_stack;
+  o->bvh_depth = c.bvh_depth;
+  o->node_bytes = (uint64_t)c.nodes.size() * sizeof(float);
+  return RT2_OK;
+}
+
+int rt2_scene_materials(const rt2_scene* s, float* out, int cap) {
+  if (!s) return Fail(RT2_ERR_INVALID, "null scene");
+  int n = (int)s->scene.materials.size();
+  for (int i = 0; i < n && i < cap && out; i++) {
+    const MaterialDesc& m = s->scene.materials[(size_t)i];
+    float* r = out + 8 * i;
+    r[0] = (float)m.type;
+    r[1] = m.albedo.x;
+    r[2] = m.albedo.y;
+    r[3] = m.albedo.z;
+    r[4] = m.fuzz;
+    r[5] = m.refraction_index;
+    r[6] = (float)m.tex_idx;
+    r[7] = 0;
+  }
+  return n;
+}
+
+int rt2_scene_textures(const rt2_scene* s, float* out, int cap) {
+  if (!s) return Fail(RT2_ERR_INVALID, "null scene");
+  int n = (int)s->scene.textures.size();
+  for (int i = 0; i < n && i < cap && out; i++) {
+    const TextureDesc& t = s->scene.textures[(size_t)i];
+    float* r = out + 8 * i;
+    r[0] = (float)t.type;
+    r[1] = t.albedo.x;
+    r[2] = t.albedo.y;
+    r[3] = t.albedo.z;
+    r[4] = t.type == kTexChecker ? t.inv_scale : t.scale;
+    r[5] = (float)t.even;
+    r[6] = (float)t.odd;
+    r[7] = (float)t.noise_type;
+  }
+  return n;
+}
+
+int rt2_scene_perlin(const rt2_scene* s, int tex, float* vec, int* perm) {
+  if (!s || tex < 0 || tex >= (int)s->scene.textures.size()) return Fail(RT2_ERR_INVALID, "bad texture index");
+  const TextureDesc& t = s->scene.textures[(size_t)tex];
+  if (t.type != kTexNoise) return Fail(RT2_ERR_INVALID, "not a noise texture");
+  int pc = t.point_count;
+  for (int i = 0; i < pc; i++) {
+    if (vec) Put3(vec + 3 * i, t.perlin_vec[(size_t)i]);
+    if (perm) {
+      perm[i] = t.perm_x[(size_t)i];
+      perm[pc + i] = t.perm_y[(size_t)i];
+      perm[2 * pc + i] = t.perm_z[(size_t)i];
+    }
+  }
+  return pc;
+}
+
+int rt2_scene_get_camera(const rt2_scene* s, rt2_camera_desc* o) {
+  if (!s || !o) return Fail(RT2_ERR_INVALID, "null argument");
+  const Camera& c = s->scene.cam;
+  Put3(o->center, c.center_);
+  Put3(o->look_at, c.lookat_);
+  Put3(o->view_up, c.view_up_);
+  o->vfov = c.vfov_;
+  o->defocus_angle = c.defocus_angle_;
+  o->focus_distance = c.focus_dist_;
+  return RT2_OK;
+}
+
+int rt2_scene_set_camera(rt2_scene* s, const rt2_camera_desc* c) {
+  if (!s || !c) return Fail(RT2_ERR_INVALID, "null argument");
+  Camera& cam = s->scene.cam;
+  cam.SetCenter(vec3{c->center[0], c->center[1], c->center[2]});
+  cam.SetLookAt(vec3{c->look_at[0], c->look_at[1], c->look_at[2]});
+  cam.SetViewUp(vec3{c->view_up[0], c->view_up[1], c->view_up[2]});
+  cam.SetFOV(c->vfov);
+  cam.SetDefocusAngle(c->defocus_angle);
+  cam.SetFocusDistance(c->focus_distance);
+  return RT2_OK;
+}
+
+int rt2_camera_params(const rt2_scene* s, int w, int h, int spp, float* out) {
+  if (!s || !out || w <= 0 || h <= 0 || spp <= 0) return Fail(RT2_ERR_INVALID, "bad camera query");
+  Camera c = s->scene.cam;
+  c.SetDims(w, h);
+  c.SetSamplesPerPixel(spp);
+  CameraParams p = c.Params();
+  memcpy(out, p.pixel00, 3 * sizeof(float));
+  memcpy(out + 3, p.du, 3 * sizeof(float));
+  memcpy(out + 6, p.dv, 3 * sizeof(float));
+  memcpy(out + 9, p.center, 3 * sizeof(float));
+  memcpy(out + 12, p.defocus_u, 3 * sizeof(float));
+  memcpy(out + 15, p.defocus_v, 3 * sizeof(float));
+  out[18] = p.defocus_angle;
+  out[19] = p.recip_sqrt_spp;
+  out[20] = (float)p.sqrt_spp;
+  return RT2_OK;
+}
+
+int rt2_camera_load(const char* path, rt2_camera_desc* o) {
+  if (!path || !o) return Fail(RT2_ERR_INVALID, "null argument");
+  Camera c;
+  std::string err;
+  if (!LoadCameraFile(path, c, err)) return Fail(RT2_ERR_IO, err);
+  Put3(o->center, c.center_);
+  Put3(o->look_at, c.lookat_);
+  Put3(o->view_up, c.view_up_);
+  o->vfov = c.vfov_;
+  o->defocus_angle = c.defocus_angle_;
+  o->focus_distance = c.focus_dist_;
+  return RT2_OK;
+}
+
+int rt2_camera_write(const rt2_camera_desc* d, const char* path) {
+  if (!d || !path) return Fail(RT2_ERR_INVALID, "null argument");
+  Camera c;
+  c.SetCenter(vec3{d->center[0], d->center[1], d->center[2]});
+  c.SetLookAt(vec3{d->look_at[0], d->look_at[1], d->look_at[2]});
+  c.SetViewUp(vec3{d->view_up[0], d->view_up[1], d->view_up[2]});
+  c.SetFOV(d->vfov);
+  c.SetDefocusAngle(d->defocus_angle);
+  c.SetFocusDistance(d->focus_distance);
+  std::string err;
+  if (!WriteCameraFile(c, path, err)) return Fail(RT2_ERR_IO, err);
+  return RT2_OK;
+}
+
+int rt2_settings_load(const char* path, rt2_app_settings* o) {
+  if (!path || !o) return Fail(RT2_ERR_INVALID, "null argument");
+  AppSettings a;
+  std::string err;
+  if (!LoadAppSettingsFile(path, a, err)) return Fail(RT2_ERR_IO, err);
+  o->render_once = a.render_once;
+  o->save_after_render_once = a.save_after_render_once;
+  o->num_samples = a.num_samples;
+  o->max_depth = a.max_depth;
+  o->render_window = a.render_window;
+  return RT2_OK;
+}
+
+int rt2_tracer_create(const rt2_scene* s, int device, rt2_tracer** out) {
+  if (!s || !out) return Fail(RT2_ERR_INVALID, "rt2_tracer_create: null argument");
+  *out = nullptr;
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess || ndev == 0) return Fail(RT2_ERR_HIP, "no HIP device available");
+  if (device < 0 || device >= ndev) return Fail(RT2_ERR_INVALID, "device index out of range");
+  auto t = std::make_unique<rt2_tracer>();
+  t->device = device;
+  HIP_TRY(hipSetDevice(device));
+  HIP_TRY(hipStreamCreateWithFlags(&t->own_stream, hipStreamNonBlocking));
+  t->stream = t->own_stream;
+  const CompiledScene& c = s->compiled;
+  int rc;
+  if ((rc = Upload(&t->d_nodes, c.nodes.data(), c.nodes.size() * sizeof(float))) != RT2_OK) return rc;
+  std::vector<float> mats = c.materials;
+  if (mats.empty()) mats.assign(8, 0.0f);
+  if ((rc = Upload(&t->d_materials, mats.data(), mats.size() * sizeof(float))) != RT2_OK) return rc;
+  if ((rc = Upload(&t->d_textures, c.textures.data(), c.textures.size() * sizeof(float))) != RT2_OK) return rc;
+  if ((rc = Upload(&t->d_perlin_vec, c.perlin_vec.data(), c.perlin_vec.size() * sizeof(float))) != RT2_OK) return rc;
+  if ((rc = Upload(&t->d_perlin_perm, c.perlin_perm.data(), c.perlin_perm.size() * sizeof(int))) != RT2_OK) return rc;
+  HIP_TRY(hipMalloc(&t->d_work, 64));
+  HIP_TRY(hipMalloc(&t->d_stats, 16 * sizeof(unsigned long long)));
+  HIP_TRY(hipMemset(t->d_stats, 0, 16 * sizeof(unsigned long long)));
+  t->root = c.root;
+  Put3(t->background, s->scene.background);
+  t->camera = s->scene.cam;
+  int cus = 0;
+  HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+  t->grid = cus * RenderBlocksPerCU(false);
+  // App.cpp:122-125,157: scene dims when present, else the window default 1600x900
+  int w = s->scene.dims_x > 0 && s->scene.dims_y > 0 ? s->scene.dims_x : 1600;
+  int h = s->scene.dims_x > 0 && s->scene.dims_y > 0 ? s->scene.dims_y : 900;
+  rt2_tracer* raw = t.release();
+  rc = rt2_tracer_on_resize(raw, w, h);
+  if (rc != RT2_OK) {
+    rt2_tracer_destroy(raw);
+    return rc;
+  }
+  *out = raw;
+  return RT2_OK;
+}
+
+void rt2_tracer_destroy(rt2_tracer* t) {
+  if (!t) return;
+  (void)hipSetDevice(t->device);
+  if (t->stream) (void)hipStreamSynchronize(t->stream);
+  for (auto& pr : t->pending) {
+    (void)hipEventDestroy(pr.first);
+    (void)hipEventDestroy(pr.second);
+  }
+  for (hipEvent_t e : t->event_pool) (void)hipEventDestroy(e);
+  FreeFrame(t);
+  (void)hipFree(t->d_nodes);
+  (void)hipFree(t->d_materials);
+  (void)hipFree(t->d_textures);
+  (void)hipFree(t->d_perlin_vec);
+  (void)hipFree(t->d_perlin_perm);
+  (void)hipFree(t->d_work);
+  (void)hipFree(t->d_stats);
+  if (t->own_stream) (void)hipStreamDestroy(t->own_stream);
+  delete t;
+}
+
+int rt2_tracer_set_stream(rt2_tracer* t, void* s) {
+  if (!t) return Fail(RT2_ERR_INVALID, "null tracer");
+  int rc = Sync(t);
+  if (rc != RT2_OK) return rc;
+  t->stream = s ? (hipStream_t)s : t->own_stream;
+  return RT2_OK;
+}
+
+int rt2_tracer_set_max_depth(rt2_tracer* t, int d) {
+  if (!t) return Fail(RT2_ERR_INVALID, "null tracer");
+  t->max_depth = d;
+  return RT2_OK;
+}
+
+int rt2_tracer_set_samples_per_pixel(rt2_tracer* t, int spp) {
+  if (!t || spp <= 0) return Fail(RT2_ERR_INVALID, "samples_per_pixel must be positive");
+  t->camera.SetSamplesPerPixel(spp);
+  return RT2_OK;
+}
+
+int rt2_tracer_set_seed(rt2_tracer* t, uint64_t seed) {
+  if (!t) return Fail(RT2_ERR_INVALID, "null tracer");
+  t->seed = seed;
+  return RT2_OK;
+}
+
+int rt2_tracer_set_partition(rt2_tracer* t, int band_h, int rank, int world) {
+  if (!t || band_h < 0 || world < 1 || rank < 0 || rank >= world)
+    return Fail(RT2_ERR_INVALID, "bad partition (need band_h >= 0, 0 <= rank < world)");
+  int rc = Sync(t);
+  if (rc != RT2_OK) return rc;
+  t->band_h = band_h;
+  t->rank = rank;
+  t->world = world;
+  if ((rc = Realloc(t)) != RT2_OK) return rc;
+  return ResetFrame(t);
+}
+
+int rt2_tracer_set_launch_frames(rt2_tracer* t, int n) {
+  if (!t || n < 0) return Fail(RT2_ERR_INVALID, "frames_per_launch must be >= 0");
+  t->launch_frames = n;
+  return RT2_OK;
+}
+
+int rt2_tracer_on_resize(rt2_tracer* t, int w, int h) {
+  if (!t || w <= 0 || h <= 0) return Fail(RT2_ERR_INVALID, "dims must be positive");
+  int rc = Sync(t);
+  if (rc != RT2_OK) return rc;
+  t->width = w;
+  t->height = h;
+  t->camera.SetDims(w, h);
+  if ((rc = Realloc(t)) != RT2_OK) return rc;
+  return ResetFrame(t);
+}
+
+int rt2_tracer_reset(rt2_tracer* t) {
+  if (!t) return Fail(RT2_ERR_INVALID, "null tracer");
+  HIP_TRY(hipSetDevice(t->device));
+  return ResetFrame(t);
+}
+
+int rt2_tracer_render(rt2_tracer* t, int n_frames) {
+  if (!t || n_frames < 0) return Fail(RT2_ERR_INVALID, "n_frames must be >= 0");
+  if (n_frames == 0 || t->local_rows == 0) {
+    t->frame_idx += n_frames;
+    return RT2_OK;
+  }
+  if ((int64_t)t->frame_idx + n_frames > 0x7FFFFFFF) return Fail(RT2_ERR_INVALID, "frame index overflow");
+  HIP_TRY(hipSetDevice(t->device));
+  RenderParams p;
+  memset(&p, 0, sizeof(p));
+  p.nodes = t->d_nodes;
+  p.materials = t->d_materials;
+  p.textures = t->d_textures;
+  p.perlin_vec = t->d_perlin_vec;
+  p.perlin_perm = t->d_perlin_perm;
+  p.root = t->root;
+  memcpy(p.background, t->background, sizeof(p.background));
+  p.cam = t->camera.Params();  // RayTracer::Update → camera->Update() (RayTracer.cpp:56)
+  if (p.cam.sqrt_spp <= 0) return Fail(RT2_ERR_INVALID, "samples_per_pixel gives sqrt_spp = 0");
+  p.width = t->width;
+  p.height = t->height;
+  p.local_rows = t->local_rows;
+  p.band_h = t->band_h > 0 ? t->band_h : t->height;
+  p.rank = t->rank;
+  p.world = t->world;
+  p.tiles_x = (t->width + 7) / 8;
+  p.n_items = (uint32_t)p.tiles_x * (uint32_t)((t->local_rows + 7) / 8) * 64u;
+  p.max_depth = t->max_depth;
+  p.seed_lo = (uint32_t)t->seed;
+  p.seed_hi = (uint32_t)(t->seed >> 32);
+  p.accum = t->d_accum;
+  p.pixels = t->d_pixels;
+  p.ray_counts = t->d_ray_counts;
+  p.work_counter = t->d_work;
+  p.stats = t->d_stats;
+  int chunk = t->launch_frames > 0 ? t->launch_frames : n_frames;
+  int grid = t->grid;
+  if (t->stats_on) {
+    int cus = 0;
+    HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, t->device));
+    grid = cus * RenderBlocksPerCU(true);
+  }
+  int64_t lanes_needed = ((int64_t)p.n_items + RenderBlockSize() - 1) / RenderBlockSize();
+  if (grid > lanes_needed) grid = (int)lanes_needed;
+  for (int done = 0; done < n_frames; done += chunk) {
+    p.frame_begin = (int)t->frame_idx;
+    p.n_frames = std::min(chunk, n_frames - done);
+    HIP_TRY(hipMemsetAsync(t->d_work, 0, sizeof(uint32_t), t->stream));
+    hipEvent_t e0 = TakeEvent(t), e1 = TakeEvent(t);
+    if (e0) HIP_TRY(hipEventRecord(e0, t->stream));
+    HIP_TRY(LaunchRender(p, t->stats_on, grid, t->stream));
+    if (e1) HIP_TRY(hipEventRecord(e1, t->stream));
+    if (e0 && e1) t->pending.emplace_back(e0, e1);
+    t->launches++;
+    t->frame_idx += p.n_frames;
+  }
+  if (t->pending.size() > 256) return DrainEvents(t);
+  return RT2_OK;
+}
+
+int rt2_tracer_update(rt2_tracer* t) { return rt2_tracer_render(t, 1); }
+
+int rt2_tracer_synchronize(rt2_tracer* t) {
+  if (!t) return Fail(RT2_ERR_INVALID, "null tracer");
+  return Sync(t);
+}
+
+int64_t rt2_tracer_frame_idx(const rt2_tracer* t) { return t ? t->frame_idx : -1; }
+
+int rt2_tracer_dims(const rt2_tracer* t, int* w, int* h) {
+  if (!t) return Fail(RT2_ERR_INVALID, "null tracer");
+  if (w) *w = t->width;
+  if (h) *h = t->height;
+  return RT2_OK;
+}
+
+int rt2_tracer_local_rows(const rt2_tracer* t) { return t ? t->local_rows : -1; }
+
+int rt2_tracer_accumulation(rt2_tracer* t, float* out) {
+  if (!t || !out) return Fail(RT2_ERR_INVALID, "null argument");
+  int rc = Sync(t);
+  if (rc != RT2_OK) return rc;
+  size_t n = (size_t)t->width * (size_t)t->local_rows;
+  if (n) HIP_TRY(hipMemcpy(out, t->d_accum, n * 3 * sizeof(float), hipMemcpyDeviceToHost));
+  return RT2_OK;
+}
+
+int rt2_tracer_non_converted_pixels(rt2_tracer* t, float* out) {
+  int rc = rt2_tracer_accumulation(t, out);
+  if (rc != RT2_OK) return rc;
+  size_t n = (size_t)t->width * (size_t)t->local_rows * 3;
+  float f = (float)t->frame_idx;  // accumulation / frame_idx_ (RayTracer.cpp:108-109)
+  for (size_t i = 0; i < n; i++) out[i] = out[i] / f;
+  return RT2_OK;
+}
+
+int rt2_tracer_pixels(rt2_tracer* t, uint8_t* out) {
+  if (!t || !out) return Fail(RT2_ERR_INVALID, "null argument");
+  int rc = Sync(t);
+  if (rc != RT2_OK) return rc;
+  size_t n = (size_t)t->width * (size_t)t->local_rows;
+  if (n) HIP_TRY(hipMemcpy(out, t->d_pixels, n * 4, hipMemcpyDeviceToHost));
+  return RT2_OK;
+}
+
+int rt2_tracer_copy_accum_device(rt2_tracer* t, void* dst, void* stream) {
+  if (!t || !dst) return Fail(RT2_ERR_INVALID, "null argument");
+  HIP_TRY(hipSetDevice(t->device));
+  hipStream_t s = stream ? (hipStream_t)stream : t->stream;
+  size_t n = (size_t)t->width * (size_t)t->local_rows;
+  if (s != t->stream) {
+    hipEvent_t e = TakeEvent(t);
+    if (!e) return Fail(RT2_ERR_HIP, "event create failed");
+    HIP_TRY(hipEventRecord(e, t->stream));
+    HIP_TRY(hipStreamWaitEvent(s, e, 0));
+    t->event_pool.push_back(e);
+  }
+  if (n) HIP_TRY(hipMemcpyAsync(dst, t->d_accum, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s));
+  return RT2_OK;
+}
+
+int rt2_tracer_enable_ray_counts(rt2_tracer* t, int on) {
+  if (!t) return Fail(RT2_ERR_INVALID, "null tracer");
+  int rc = Sync(t);
+  if (rc != RT2_OK) return rc;
+  t->ray_counts_on = on != 0;
+  if ((rc = Realloc(t)) != RT2_OK) return rc;
+  return ResetFrame(t);
+}
+
+int rt2_tracer_ray_counts(rt2_tracer* t, uint32_t* out) {
+  if (!t || !out) return Fail(RT2_ERR_INVALID, "null argument");
+  if (!t->d_ray_counts) return Fail(RT2_ERR_INVALID, "ray counts not enabled");
+  int rc = Sync(t);
+  if (rc != RT2_OK) return rc;
+  size_t n = (size_t)t->width * (size_t)t->local_rows;
+  if (n) HIP_TRY(hipMemcpy(out, t->d_ray_counts, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  return RT2_OK;
+}
+
+int rt2_tracer_enable_stats(rt2_tracer* t, int on) {
+  if (!t) return Fail(RT2_ERR_INVALID, "null tracer");
+  t->stats_on = on != 0;
+  return RT2_OK;
+}
+
+int rt2_tracer_get_stats(rt2_tracer* t, rt2_stats* o) {
+  if (!t || !o) return Fail(RT2_ERR_INVALID, "null argument");
+  int rc = Sync(t);
+  if (rc != RT2_OK) return rc;
+  unsigned long long s[16];
+  HIP_TRY(hipMemcpy(s, t->d_stats, sizeof(s), hipMemcpyDeviceToHost));
+  o->rays = s[StatsCounters::kRays];
+  o->paths = s[StatsCounters::kPaths];
+  o->bvh_tests = s[StatsCounters::kBvhTests];
+  o->quad_tests = s[StatsCounters::kQuadTests];
+  o->sphere_tests = s[StatsCounters::kSphereTests];
+  o->xform_visits = s[StatsCounters::kXformVisits];
+  o->medium_tests = s[StatsCounters::kMediumTests];
+  o->list_visits = s[StatsCounters::kListVisits];
+  o->overflow = s[StatsCounters::kCount];
+  o->launches = t->launches;
+  o->kernel_ms = t->kernel_ms;
+  return RT2_OK;
+}
+
+int rt2_tracer_reset_stats(rt2_tracer* t) {
+  if (!t) return Fail(RT2_ERR_INVALID, "null tracer");
+  int rc = Sync(t);
+  if (rc != RT2_OK) return rc;
+  HIP_TRY(hipMemset(t->d_stats, 0, 16 * sizeof(unsigned long long)));
+  t->launches = 0;
+  t->kernel_ms = 0;
+  return RT2_OK;
+}
+
+int rt2_write_image(const float* pixels, int w, int h, const char* path, int png) {
+  if (!pixels || !path || w <= 0 || h <= 0) return Fail(RT2_ERR_INVALID, "bad image arguments");
+  std::string err;
+  if (!WriteImage(pixels, w, h, path, png != 0, err)) return Fail(RT2_ERR_IO, err);
+  return RT2_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,291 @@
+// compile.cpp — flattens the host object graph (scene.h) into the node array the gfx950 kernel
+// walks (rt2_layout.h), and proves the kernel's traversal-stack bound for the scene.
+#include <cstring>
+#include <functional>
+#include <unordered_map>
+
+#include "scene.h"
+
+namespace rt2 {
+
+namespace {
+
+struct Flattener {
+  const Scene& s;
+  CompiledScene& out;
+  std::unordered_map<int, uint32_t> ref_of;  // obj index -> node ref (DAG sharing)
+  std::unordered_map<int, bool> medium_memo;
+
+  Flattener(const Scene& sc, CompiledScene& o) : s(sc), out(o) {}
+
+  uint32_t Alloc(int records) {
+    uint32_t off = (uint32_t)(out.nodes.size() / 4);
+    out.nodes.resize(out.nodes.size() + 4 * (size_t)records, 0.0f);
+    return off;
+  }
+  float* Rec(uint32_t off) { return out.nodes.data() + 4 * (size_t)off; }
+  static float Bits(uint32_t u) {
+    float f;
+    memcpy(&f, &u, 4);
+    return f;
+  }
+  void Put(uint32_t off, float a, float b, float c, float d) {
+    float* r = Rec(off);
+    r[0] = a;
+    r[1] = b;
+    r[2] = c;
+    r[3] = d;
+  }
+
+  bool HasMedium(int i) {
+    auto it = medium_memo.find(i);
+    if (it != medium_memo.end()) return it->second;
+    const Obj& o = s.objs[(size_t)i];
+    bool r = false;
+    switch (o.kind) {
+      case kMedium: r = true; break;
+      case kXform: r = HasMedium(o.child); break;
+      case kBvh: r = HasMedium(o.left) || HasMedium(o.right); break;
+      case kList:
+        for (int c : o.children) r = r || HasMedium(c);
+        break;
+      default: break;
+    }
+    medium_memo[i] = r;
+    return r;
+  }
+
+  bool IsLeafPrim(int i) const {
+    NodeKind k = s.objs[(size_t)i].kind;
+    return k == kQuad || k == kSphere;
+  }
+
+  // Emits object i (children first) and returns its ref. parent_xf = enclosing XFORM ref.
+  uint32_t Emit(int i, uint32_t parent_xf, std::string& err) {
+    auto it = ref_of.find(i);
+    if (it != ref_of.end()) return it->second;
+    const Obj& o = s.objs[(size_t)i];
+    uint32_t ref = kRefNone;
+    switch (o.kind) {
+      case kQuad: {
+        uint32_t off = Alloc(kQuadRecords);
+        Put(off, o.n.x, o.n.y, o.n.z, o.d);
+        Put(off + 1, o.q.x, o.q.y, o.q.z, Bits(o.material));
+        Put(off + 2, o.u.x, o.u.y, o.u.z, 0);
+        Put(off + 3, o.v.x, o.v.y, o.v.z, 0);
+        Put(off + 4, o.w.x, o.w.y, o.w.z, 0);
+        ref = make_ref(kQuad, off);
+        out.quads++;
+        break;
+      }
+      case kSphere: {
+        uint32_t off = Alloc(kSphereRecords);
+        Put(off, o.c0.x, o.c0.y, o.c0.z, o.radius);
+        Put(off + 1, o.disp.x, o.disp.y, o.disp.z, Bits(o.material));
+        ref = make_ref(kSphere, off);
+        out.spheres++;
+        break;
+      }
+      case kList: {
+        std::vector<uint32_t> refs;
+        bool leaf_only = true;
+        for (int c : o.children) {
+          uint32_t r = Emit(c, parent_xf, err);
+          if (r == kRefNone) return kRefNone;
+          refs.push_back(r);
+          leaf_only = leaf_only && IsLeafPrim(c);
+        }
+        int recs = 1 + (int)((refs.size() + 3) / 4);
+        uint32_t off = Alloc(recs);
+        Put(off, Bits((uint32_t)refs.size()), Bits(leaf_only ? kListLeafOnly : 0u), 0, 0);
+        for (size_t k = 0; k < refs.size(); k++) Rec(off + 1 + (uint32_t)(k / 4))[k % 4] = Bits(refs[k]);
+        ref = make_ref(kList, off);
+        out.lists++;
+        break;
+      }
+      case kXform: {
+        // The XFORM's own record is allocated first so its ref can be the children's parent.
+        uint32_t off = Alloc(kXformRecords);
+        uint32_t self = make_ref(kXform, off);
+        // children of an XFORM are emitted with this XFORM as their parent; a shared child that
+        // was already emitted under another parent would get the wrong parent link
+        if (ref_of.count(o.child) && s.objs[(size_t)o.child].kind == kXform) {
+          err = "a transformed node is shared between two transforms";
+          return kRefNone;
+        }
+        uint32_t child = Emit(o.child, self, err);
+        if (child == kRefNone) return kRefNone;
+        const mat4& iv = o.inv_model;
+        const mat4& m = o.model;
+        Put(off + 0, iv[0][0], iv[0][1], iv[0][2], Bits(child));
+        Put(off + 1, iv[1][0], iv[1][1], iv[1][2], Bits(parent_xf));
+        Put(off + 2, iv[2][0], iv[2][1], iv[2][2], 0);
+        Put(off + 3, iv[3][0], iv[3][1], iv[3][2], 0);
+        Put(off + 4, m[0][0], m[0][1], m[0][2], 0);
+        Put(off + 5, m[1][0], m[1][1], m[1][2], 0);
+        Put(off + 6, m[2][0], m[2][1], m[2][2], 0);
+        Put(off + 7, m[3][0], m[3][1], m[3][2], 0);
+        ref = self;
+        out.xforms++;
+        break;
+      }
+      case kMedium: {
+        const Obj& b = s.objs[(size_t)o.child];
+        bool ok = b.kind == kQuad || b.kind == kSphere;
+        if (b.kind == kList) {
+          ok = true;
+          for (int c : b.children) ok = ok && IsLeafPrim(c);
+        }
+        if (!ok) {
+          err = "constant_medium boundary must be a quad, a sphere or a box";
+          return kRefNone;
+        }
+        uint32_t bref = Emit(o.child, parent_xf, err);
+        if (bref == kRefNone) return kRefNone;
+        uint32_t off = Alloc(kMediumRecords);
+        Put(off, o.neg_inv_density, Bits(o.material), Bits(bref), 0);
+        ref = make_ref(kMedium, off);
+        out.media++;
+        break;
+      }
+      case kBvh: {
+        uint32_t l = Emit(o.left, parent_xf, err);
+        if (l == kRefNone) return kRefNone;
+        uint32_t r;
+        if (o.left == o.right && !HasMedium(o.left)) {
+          // Span-1 leaf (BVH.cpp:18-20) tests its object twice. The second test runs on
+          // [min, rec.t] and provably leaves the hit record unchanged unless a ConstantMedium
+          // (which draws a fresh random number per call) lies below, so it is skipped.
+          r = kRefNone;
+        } else {
+          r = Emit(o.right, parent_xf, err);
+          if (r == kRefNone) return kRefNone;
+        }
+        uint32_t off = Alloc(kBvhRecords);
+        const AABB& bb = o.aabb;
+        Put(off, bb.x.min, bb.y.min, bb.z.min, Bits(l));
+        Put(off + 1, bb.x.max, bb.y.max, bb.z.max, Bits(r));
+        ref = make_ref(kBvh, off);
+        out.bvh_nodes++;
+        break;
+      }
+      default:
+        err = "unknown object kind";
+        return kRefNone;
+    }
+    ref_of[i] = ref;
+    return ref;
+  }
+
+  // Stack entries the kernel holds for this subtree once its ref has been popped.
+  int StackNeed(int i, int& depth_out) {
+    const Obj& o = s.objs[(size_t)i];
+    depth_out = 0;
+    switch (o.kind) {
+      case kBvh: {
+        int dl = 0, dr = 0;
+        int nl = StackNeed(o.left, dl);
+        int nr = StackNeed(o.right, dr);
+        depth_out = 1 + std::max(dl, dr);
+        return std::max(2, std::max(1 + nl, nr));
+      }
+      case kList: {
+        bool leaf_only = true;
+        for (int c : o.children) leaf_only = leaf_only && IsLeafPrim(c);
+        if (leaf_only) return 0;
+        int n = (int)o.children.size(), need = n;
+        for (int k = 0; k < n; k++) {
+          int d = 0;
+          need = std::max(need, (n - 1 - k) + StackNeed(o.children[(size_t)k], d));
+        }
+        return need;
+      }
+      case kXform: {
+        int d = 0;
+        return std::max(2, 1 + StackNeed(o.child, d));
+      }
+      default:
+        return 0;  // quad / sphere / medium (boundary evaluated inline)
+    }
+  }
+};
+
+void PackMaterials(const Scene& s, CompiledScene& out) {
+  for (const MaterialDesc& m : s.materials) {
+    uint32_t type = m.type, tex = m.tex_idx;
+    float ri_inv = (float)(1.0 / (double)m.refraction_index);
+    float rec[8];
+    memcpy(&rec[0], &type, 4);
+    rec[1] = m.albedo.x;
+    rec[2] = m.albedo.y;
+    rec[3] = m.albedo.z;
+    rec[4] = m.fuzz;
+    rec[5] = m.refraction_index;
+    memcpy(&rec[6], &tex, 4);
+    rec[7] = ri_inv;
+    out.materials.insert(out.materials.end(), rec, rec + 8);
+  }
+}
+
+void PackTextures(const Scene& s, CompiledScene& out) {
+  for (const TextureDesc& t : s.textures) {
+    uint32_t u[12] = {0};
+    float* f = reinterpret_cast<float*>(u);
+    u[0] = t.type;
+    f[1] = t.albedo.x;
+    f[2] = t.albedo.y;
+    f[3] = t.albedo.z;
+    f[4] = t.type == kTexChecker ? t.inv_scale : t.scale;
+    u[5] = t.even;
+    u[6] = t.odd;
+    u[7] = (uint32_t)t.noise_type;
+    if (t.type == kTexNoise) {
+      u[8] = (uint32_t)(out.perlin_vec.size() / 4);
+      u[9] = (uint32_t)out.perlin_perm.size();
+      u[10] = (uint32_t)t.point_count;
+      for (const vec3& g : t.perlin_vec) {
+        out.perlin_vec.push_back(g.x);
+        out.perlin_vec.push_back(g.y);
+        out.perlin_vec.push_back(g.z);
+        out.perlin_vec.push_back(0.0f);
+      }
+      out.perlin_perm.insert(out.perlin_perm.end(), t.perm_x.begin(), t.perm_x.end());
+      out.perlin_perm.insert(out.perlin_perm.end(), t.perm_y.begin(), t.perm_y.end());
+      out.perlin_perm.insert(out.perlin_perm.end(), t.perm_z.begin(), t.perm_z.end());
+    }
+    out.textures.insert(out.textures.end(), f, f + 12);
+  }
+}
+
+}  // namespace
+
+bool CompileScene(const Scene& s, CompiledScene& out, std::string& err) {
+  out = CompiledScene();
+  if (s.root < 0) {
+    err = "scene has no BVH root";
+    return false;
+  }
+  Flattener fl(s, out);
+  out.root = fl.Emit(s.root, kRefNone, err);
+  if (out.root == kRefNone) return false;
+  int depth = 0;
+  out.max_stack = std::max(1, fl.StackNeed(s.root, depth));
+  out.bvh_depth = depth;
+  if (out.max_stack > kTraversalStack) {
+    err = "scene needs a traversal stack of " + std::to_string(out.max_stack) + " entries (kernel has " +
+          std::to_string(kTraversalStack) + ")";
+    return false;
+  }
+  if (out.nodes.size() / 4 > kOffsetMask) {
+    err = "scene too large for 28-bit node offsets";
+    return false;
+  }
+  PackMaterials(s, out);
+  PackTextures(s, out);
+  if (out.perlin_vec.empty()) out.perlin_vec.assign(4, 0.0f);
+  if (out.perlin_perm.empty()) out.perlin_perm.assign(1, 0);
+  if (out.textures.empty()) out.textures.assign(12, 0.0f);
+  return true;
+}
+
+}  // namespace rt2

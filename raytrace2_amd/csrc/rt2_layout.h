@@ -1,0 +1,96 @@
+// rt2_layout.h — layout of the flattened scene program in HBM and of the render launch
+// parameters. Shared by the host scene compiler (compile.cpp) and the gfx950 kernel
+// (render.hip). Plain POD; no HIP or torch types.
+//
+// The scene is one array of 16-byte records ("nodes", float4 units). A node reference packs the
+// node kind in bits 28..31 and the float4 offset in bits 0..27, so a parent knows what it is about
+// to fetch. Kinds mirror the reference's Hittable implementations:
+//   kBvh    BVHNode            (BVH.cpp:10-55)          2 records
+//   kQuad   Quad               (Quad.cpp:19-43)         5 records
+//   kSphere Sphere (moving)    (Sphere.cpp:7-37)        2 records
+//   kList   HittableList       (HittableList.cpp:8-22)  1 + ceil(n/4) records
+//   kXform  TransformedHittable(Transform.cpp:13-88)    8 records
+//   kMedium ConstantMedium     (ConstantMedium.cpp:14-58) 1 record
+#pragma once
+#include <stdint.h>
+
+namespace rt2 {
+
+enum NodeKind : uint32_t {
+  kBvh = 0,
+  kQuad = 1,
+  kSphere = 2,
+  kList = 3,
+  kXform = 4,
+  kMedium = 5,
+  kXformExit = 6,  // traversal-stack marker only (never stored in the node array)
+};
+
+constexpr uint32_t kRefNone = 0xFFFFFFFFu;
+constexpr uint32_t kOffsetMask = 0x0FFFFFFFu;
+inline constexpr uint32_t make_ref(uint32_t kind, uint32_t off) { return (kind << 28) | off; }
+
+// Record layouts (each line one float4; "(bits)" = uint32 stored with __float_as_uint):
+//  BVH   : (min.xyz, left_ref bits) (max.xyz, right_ref bits)  right_ref = kRefNone when a
+//          span-1 leaf's duplicate test is provably a no-op (no medium below it).
+//  QUAD  : (n.xyz, D) (q.xyz, material bits) (u.xyz, 0) (v.xyz, 0) (w.xyz, 0)
+//  SPHERE: (c0.xyz, radius) (displacement.xyz, material bits)
+//  LIST  : (count bits, flags bits, 0, 0) then child refs, 4 per record. flags bit0 = every
+//          child is a QUAD or SPHERE (iterated inline, no stack traffic).
+//  XFORM : (invM col0.xyz, child_ref bits) (invM col1.xyz, parent_xform_ref bits)
+//          (invM col2.xyz, 0) (invM col3.xyz, 0) (M col0.xyz,0) (M col1.xyz,0) (M col2.xyz,0) (M col3.xyz,0)
+//  MEDIUM: (neg_inv_density, material bits, boundary_ref bits, 0)
+constexpr uint32_t kListLeafOnly = 1u;
+
+constexpr int kBvhRecords = 2, kQuadRecords = 5, kSphereRecords = 2, kXformRecords = 8, kMediumRecords = 1;
+
+// Materials: 2 records each: (type bits, albedo.xyz) (fuzz, refraction_index, tex_idx bits, 1/ri)
+enum MaterialType : uint32_t {
+  kMatMetal = 0,
+  kMatLambertian = 1,
+  kMatDielectric = 2,
+  kMatTexture = 3,
+  kMatDiffuseLight = 4,
+  kMatIsotropic = 5,
+};
+// Textures: 3 records each: (type bits, albedo.xyz) (inv_scale|scale, even bits, odd bits,
+// noise_type bits) (perlin vec offset bits, perlin perm offset bits, point_count bits, 0)
+enum TextureType : uint32_t { kTexSolid = 0, kTexChecker = 1, kTexNoise = 2 };
+
+constexpr int kTraversalStack = 24;  // entries per lane (LDS); compile.cpp proves the bound
+
+struct CameraParams {
+  float pixel00[3], du[3], dv[3], center[3], defocus_u[3], defocus_v[3];
+  float defocus_angle;
+  float recip_sqrt_spp;
+  int sqrt_spp;
+};
+
+struct StatsCounters {  // u64 slots written by the kernel
+  enum { kRays = 0, kBvhTests, kQuadTests, kSphereTests, kXformVisits, kMediumTests, kListVisits, kPaths, kCount };
+};
+
+struct RenderParams {
+  const void* nodes;      // float4[]
+  const void* materials;  // float4[]
+  const void* textures;   // float4[]
+  const void* perlin_vec; // float4[]
+  const int* perlin_perm;
+  uint32_t root;
+  float background[3];
+  CameraParams cam;
+  int width, height;       // global image
+  int local_rows;          // rows owned by this rank
+  int band_h, rank, world; // interleaved row bands: global band b -> rank b % world
+  int tiles_x;             // ceil(width / 8)
+  uint32_t n_items;        // tiles_x * ceil(local_rows / 8) * 64
+  int frame_begin, n_frames, max_depth;
+  uint32_t seed_lo, seed_hi;
+  float* accum;            // float3 per local pixel (row-major local rows)
+  uint8_t* pixels;         // RGBA8 per local pixel (RayTracer::Pixels)
+  uint32_t* ray_counts;    // optional: += rays per local pixel
+  uint32_t* work_counter;  // zeroed before launch
+  unsigned long long* stats;  // StatsCounters::kCount slots
+};
+
+}  // namespace rt2

@@ -1,0 +1,49 @@
+"""Shared helpers: product (GPU, through the C ABI) and oracle (CPU restatement) renders."""
+import numpy as np
+
+from conftest import scene_path
+
+SEED = 0x5EED2024
+
+
+def gpu_render(name, w, h, spp, frames, *, seed=SEED, max_depth=50, band_h=0, rank=0, world=1,
+               launch_frames=0, updates=False, stats=False):
+    import torch  # noqa: F401
+    import raytrace2_amd as R
+    sc = R.Scene(scene_path(name), seed)
+    tr = R.RayTracer(sc, 0)
+    tr.set_seed(seed)
+    tr.SetSamplesPerPixel(spp)
+    tr.max_depth = max_depth
+    tr.enable_ray_counts(True)
+    if stats:
+        tr.enable_stats(True)
+    tr.OnResize((w, h))
+    if world > 1 or band_h:
+        tr.set_partition(band_h, rank, world)
+    if launch_frames:
+        tr.set_launch_frames(launch_frames)
+    if updates:
+        for _ in range(frames):
+            tr.Update(sc)
+    else:
+        tr.Render(frames)
+    acc = tr.Accumulation()
+    rc = tr.ray_counts()
+    st = tr.stats()
+    px = tr.Pixels()
+    tr.close()
+    return acc, rc, st, px
+
+
+def oracle_render(name, w, h, spp, frames, *, seed=SEED, max_depth=50, band_h=0, rank=0, world=1,
+                  forward=True, threads=0):
+    from oracle.oracle import OracleScene
+    o = OracleScene(scene_path(name), seed)
+    acc, rc, cnt = o.render(w, h, spp, frames, max_depth=max_depth, band_h=band_h, rank=rank, world=world,
+                            forward=forward, threads=threads)
+    return acc, rc, cnt
+
+
+def rmse(a, b):
+    return float(np.sqrt(np.mean((np.asarray(a, np.float64) - np.asarray(b, np.float64)) ** 2)))
