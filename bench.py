@@ -71,7 +71,10 @@ def main():
     t0 = time.perf_counter()
     sc = R.Scene(scene_file, a.seed)
     tr = R.RayTracer(sc, local_rank)
-    stream = torch.cuda.current_stream(dev)
+    # a dedicated (non-null) torch stream shared with the tracer, so torch events and RCCL calls
+    # order against the render kernels
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     tr.set_stream(stream.cuda_stream)
     tr.set_seed(a.seed)
     tr.max_depth = a.max_depth
@@ -217,7 +220,8 @@ def main():
             "cpu_baseline": cpu,
             "detail": {"rays": int(rays_total), "stream_ms": round(stream_ms, 2),
                        "kernel_ms_per_step": round(kernel_ms / a.steps, 2), "launches": launches,
-                       "setup_s": round(setup_s, 3),
+                       "variant_features": hex(tr.last_variant_features()) if hasattr(tr, "last_variant_features") else None,
+                       "setup_s": round(setup_s, 3), "stamps": st.get("stamps"),
                        "rays_per_sample": round(rays_total / (a.steps * a.spp * a.width * a.height), 4)},
         }
         if cpu:

@@ -7,7 +7,7 @@ import os
 import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "librt2.so")
+LIB_PATH = os.environ.get("RT2_LIB") or os.path.join(_HERE, "lib", "librt2.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "rt2.h")
 
 RT2_OK = 0
@@ -48,10 +48,14 @@ class AppSettings(ctypes.Structure):
 class Stats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in
                 ("rays", "paths", "bvh_tests", "quad_tests", "sphere_tests", "xform_visits",
-                 "medium_tests", "list_visits", "overflow", "launches")] + [("kernel_ms", ctypes.c_double)]
+                 "medium_tests", "list_visits", "overflow", "launches")] + [("kernel_ms", ctypes.c_double),
+                                                                           ("stamps", ctypes.c_uint64 * 4)]
 
     def as_dict(self):
-        return {n: (getattr(self, n) if n == "kernel_ms" else int(getattr(self, n))) for n, _ in self._fields_}
+        d = {n: (getattr(self, n) if n == "kernel_ms" else int(getattr(self, n))) for n, _ in self._fields_
+             if n != "stamps"}
+        d["stamps"] = [int(x) for x in self.stamps]
+        return d
 
 
 def declared_symbols(header: str = HEADER_PATH):

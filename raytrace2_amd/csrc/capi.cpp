@@ -3,6 +3,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -12,9 +13,13 @@
 #include "scene.h"
 
 namespace rt2 {
-hipError_t LaunchRender(const RenderParams& p, bool stats, int grid, hipStream_t stream);
-int RenderBlocksPerCU(bool stats);
+hipError_t LaunchRender(const RenderParams& p, int variant, bool stats, int grid, hipStream_t stream);
+int RenderBlocksPerCU(int variant, int mode, bool stats, size_t lds_bytes);
+int RenderMode(const RenderParams& p);
 int RenderBlockSize();
+int RenderVariant(uint32_t features);
+uint32_t RenderVariantFeatures(int v);
+size_t RenderLdsBytes(const RenderParams& p);
 bool WriteImage(const float* pixels, int w, int h, const std::string& path, bool png, std::string& err);
 }  // namespace rt2
 
@@ -35,7 +40,15 @@ struct rt2_tracer {
   void* d_textures = nullptr;
   void* d_perlin_vec = nullptr;
   int* d_perlin_perm = nullptr;
+  void* d_lin = nullptr;
+  uint32_t lin_len = 0;
+  bool use_linear = true;
   uint32_t root = kRefNone;
+  uint32_t node_records = 0;
+  uint32_t features = 0;
+  int max_stack = 1;
+  bool use_lds = true;
+  int cus = 0;
   float background[3] = {0, 0, 0};
   Camera camera;  // RayTracer::camera (a copy of the scene camera)
   // frame buffers (local rows)
@@ -52,7 +65,8 @@ struct rt2_tracer {
   int max_depth = 50;
   uint64_t seed = 0x5EED2024ull;
   int launch_frames = 0;
-  int grid = 0;
+  int last_variant = -1;
+  int last_grid = 0;
   uint64_t launches = 0;
   double kernel_ms = 0;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;  // per-launch timing events
@@ -360,15 +374,22 @@ int rt2_tracer_create(const rt2_scene* s, int device, rt2_tracer** out) {
   if ((rc = Upload(&t->d_textures, c.textures.data(), c.textures.size() * sizeof(float))) != RT2_OK) return rc;
   if ((rc = Upload(&t->d_perlin_vec, c.perlin_vec.data(), c.perlin_vec.size() * sizeof(float))) != RT2_OK) return rc;
   if ((rc = Upload(&t->d_perlin_perm, c.perlin_perm.data(), c.perlin_perm.size() * sizeof(int))) != RT2_OK) return rc;
+  if (!c.lin.empty()) {
+    if ((rc = Upload(&t->d_lin, c.lin.data(), c.lin.size() * sizeof(uint32_t))) != RT2_OK) return rc;
+    t->lin_len = (uint32_t)(c.lin.size() / 4);
+  }
   HIP_TRY(hipMalloc(&t->d_work, 64));
   HIP_TRY(hipMalloc(&t->d_stats, 16 * sizeof(unsigned long long)));
   HIP_TRY(hipMemset(t->d_stats, 0, 16 * sizeof(unsigned long long)));
   t->root = c.root;
+  t->node_records = (uint32_t)(c.nodes.size() / 4);
+  t->features = c.features;
+  t->max_stack = c.max_stack;
   Put3(t->background, s->scene.background);
   t->camera = s->scene.cam;
-  int cus = 0;
-  HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-  t->grid = cus * RenderBlocksPerCU(false);
+  HIP_TRY(hipDeviceGetAttribute(&t->cus, hipDeviceAttributeMultiprocessorCount, device));
+  if (const char* e = getenv("RT2_NO_LDS")) t->use_lds = e[0] == '0';
+  if (const char* e = getenv("RT2_NO_LINEAR")) t->use_linear = e[0] == '0';
   // App.cpp:122-125,157: scene dims when present, else the window default 1600x900
   int w = s->scene.dims_x > 0 && s->scene.dims_y > 0 ? s->scene.dims_x : 1600;
   int h = s->scene.dims_x > 0 && s->scene.dims_y > 0 ? s->scene.dims_y : 900;
@@ -397,6 +418,7 @@ void rt2_tracer_destroy(rt2_tracer* t) {
   (void)hipFree(t->d_textures);
   (void)hipFree(t->d_perlin_vec);
   (void)hipFree(t->d_perlin_perm);
+  (void)hipFree(t->d_lin);
   (void)hipFree(t->d_work);
   (void)hipFree(t->d_stats);
   if (t->own_stream) (void)hipStreamDestroy(t->own_stream);
@@ -499,22 +521,26 @@ int rt2_tracer_render(rt2_tracer* t, int n_frames) {
   p.ray_counts = t->d_ray_counts;
   p.work_counter = t->d_work;
   p.stats = t->d_stats;
+  p.stack_depth = t->max_stack;
+  bool lds = t->use_lds && (size_t)t->node_records * 16 <= (size_t)kLdsSceneBytesMax;
+  p.lds_nodes = lds ? t->node_records : 0u;
+  p.lin = t->d_lin;
+  p.lin_len = t->use_linear ? t->lin_len : 0u;
+  uint32_t feats = t->features | (p.cam.defocus_angle > 0.0f ? (uint32_t)kFeatDefocus : 0u);
+  int variant = RenderVariant(feats);
+  int grid = t->cus * RenderBlocksPerCU(variant, RenderMode(p), t->stats_on, RenderLdsBytes(p));
+  int64_t blocks_needed = ((int64_t)p.n_items + RenderBlockSize() - 1) / RenderBlockSize();
+  if (grid > blocks_needed) grid = (int)blocks_needed;
+  t->last_variant = variant;
+  t->last_grid = grid;
   int chunk = t->launch_frames > 0 ? t->launch_frames : n_frames;
-  int grid = t->grid;
-  if (t->stats_on) {
-    int cus = 0;
-    HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, t->device));
-    grid = cus * RenderBlocksPerCU(true);
-  }
-  int64_t lanes_needed = ((int64_t)p.n_items + RenderBlockSize() - 1) / RenderBlockSize();
-  if (grid > lanes_needed) grid = (int)lanes_needed;
   for (int done = 0; done < n_frames; done += chunk) {
     p.frame_begin = (int)t->frame_idx;
     p.n_frames = std::min(chunk, n_frames - done);
     HIP_TRY(hipMemsetAsync(t->d_work, 0, sizeof(uint32_t), t->stream));
     hipEvent_t e0 = TakeEvent(t), e1 = TakeEvent(t);
     if (e0) HIP_TRY(hipEventRecord(e0, t->stream));
-    HIP_TRY(LaunchRender(p, t->stats_on, grid, t->stream));
+    HIP_TRY(LaunchRender(p, variant, t->stats_on, grid, t->stream));
     if (e1) HIP_TRY(hipEventRecord(e1, t->stream));
     if (e0 && e1) t->pending.emplace_back(e0, e1);
     t->launches++;
@@ -625,6 +651,7 @@ int rt2_tracer_get_stats(rt2_tracer* t, rt2_stats* o) {
   o->medium_tests = s[StatsCounters::kMediumTests];
   o->list_visits = s[StatsCounters::kListVisits];
   o->overflow = s[StatsCounters::kCount];
+  for (int k = 0; k < 4; k++) o->stamps[k] = s[9 + k];
   o->launches = t->launches;
   o->kernel_ms = t->kernel_ms;
   return RT2_OK;

@@ -101,6 +101,7 @@ struct Flattener {
         for (size_t k = 0; k < refs.size(); k++) Rec(off + 1 + (uint32_t)(k / 4))[k % 4] = Bits(refs[k]);
         ref = make_ref(kList, off);
         out.lists++;
+        if (!leaf_only) out.features |= kFeatGenList;
         break;
       }
       case kXform: {
@@ -175,6 +176,42 @@ struct Flattener {
     }
     ref_of[i] = ref;
     return ref;
+  }
+
+  // Threaded program (rt2_layout.h): pre-order of the tree the reference traverses. Returns
+  // false when the program would exceed kLinearMaxSteps.
+  bool Linearize(int i, uint32_t parent_xf, std::vector<uint32_t>& lin) {
+    if (lin.size() / 4 >= (size_t)kLinearMaxSteps) return false;
+    const Obj& o = s.objs[(size_t)i];
+    uint32_t ref = ref_of.at(i);
+    uint32_t off = ref & kOffsetMask;
+    auto emit = [&](uint32_t kind, uint32_t rec, uint32_t aux) {
+      lin.insert(lin.end(), {kind, 0u, rec, aux});
+      return lin.size() / 4 - 1;
+    };
+    switch (o.kind) {
+      case kBvh: {
+        size_t me = emit(kBvh, off, 0);
+        if (!Linearize(o.left, parent_xf, lin)) return false;
+        if (!(o.left == o.right && !HasMedium(o.left))) {
+          if (!Linearize(o.right, parent_xf, lin)) return false;
+        }
+        lin[4 * me + 1] = (uint32_t)(lin.size() / 4);
+        return true;
+      }
+      case kList:
+        for (int c : o.children)
+          if (!Linearize(c, parent_xf, lin)) return false;
+        return true;
+      case kXform:
+        emit(kXform, off, 0);
+        if (!Linearize(o.child, ref, lin)) return false;
+        emit(kXformExit, off, parent_xf);
+        return true;
+      default:  // quad, sphere, medium (boundary evaluated inline)
+        emit(o.kind, off, 0);
+        return lin.size() / 4 <= (size_t)kLinearMaxSteps;
+    }
   }
 
   // Stack entries the kernel holds for this subtree once its ref has been popped.
@@ -280,8 +317,32 @@ bool CompileScene(const Scene& s, CompiledScene& out, std::string& err) {
     err = "scene too large for 28-bit node offsets";
     return false;
   }
+  if (!fl.Linearize(s.root, kRefNone, out.lin)) out.lin.clear();
+  // Quad runs: for a quad step, aux = number of consecutive quad steps starting there with no
+  // skip target inside the run (so every lane that reaches the run's first step walks all of it).
+  {
+    size_t n = out.lin.size() / 4;
+    std::vector<char> entry(n + 1, 0);
+    for (size_t i = 0; i < n; i++)
+      if (out.lin[4 * i] == kBvh) entry[out.lin[4 * i + 1]] = 1;
+    for (size_t i = n; i-- > 0;) {
+      if (out.lin[4 * i] != kQuad) continue;
+      uint32_t run = 1;
+      if (i + 1 < n && out.lin[4 * (i + 1)] == kQuad && !entry[i + 1]) run = out.lin[4 * (i + 1) + 3] + 1;
+      out.lin[4 * i + 3] = run;
+    }
+  }
   PackMaterials(s, out);
   PackTextures(s, out);
+  if (out.spheres) out.features |= kFeatSphere;
+  if (out.media) out.features |= kFeatMedium;
+  if (out.xforms) out.features |= kFeatXform;
+  for (const MaterialDesc& m : s.materials)
+    if (m.type == kMatMetal || m.type == kMatDielectric) out.features |= kFeatSpecular;
+  for (const TextureDesc& t : s.textures) {
+    if (t.type == kTexNoise) out.features |= kFeatNoise;
+    if (t.type == kTexChecker) out.features |= kFeatChecker;
+  }
   if (out.perlin_vec.empty()) out.perlin_vec.assign(4, 0.0f);
   if (out.perlin_perm.empty()) out.perlin_perm.assign(1, 0);
   if (out.textures.empty()) out.textures.assign(12, 0.0f);

@@ -12,11 +12,14 @@
 //    frame in the same iteration (path regeneration), so lanes never idle inside a wave until
 //    their pixel is done;
 //  * pixels are handed out in 8x8 tiles by a wave-aggregated atomic: __ballot of the lanes that
-//    need work, one atomicAdd per wave, mbcnt-style prefix for each lane's slot;
-//  * the traversal stack lives in LDS (kTraversalStack entries per lane, lane-major columns, so a
-//    wave's push/pop is one conflict-free ds_write/ds_read);
-//  * the flattened scene (rt2_layout.h) is read with 16-byte loads; it is small and shared by
-//    every lane, so it is served from L1/L2.
+//    need work, one atomicAdd per wave, a popcount prefix for each lane's slot;
+//  * the traversal stack lives in LDS (lane-major columns: a wave's push/pop is one
+//    conflict-free ds_write/ds_read); scenes up to kLdsSceneBytesMax are staged in LDS as well;
+//  * traversal carries only (t, primitive ref, transform ref) of the closest hit; the hit point,
+//    normal and material are computed once for the winning primitive (bit-identical to computing
+//    them at every candidate hit, as the reference does);
+//  * the kernel is instantiated per scene feature set (rt2_layout.h Feature), so code for absent
+//    primitive / material / texture kinds costs no registers in the variant that runs.
 //
 // Numerics: compiled with -ffp-contract=off; fp32 division and sqrt are correctly rounded (HIP
 // default). Every expression repeats the reference's operation order, so results match the
@@ -33,6 +36,25 @@ namespace rt2 {
 namespace dev {
 
 constexpr int kBlock = 256;
+
+// Ablation switches for performance experiments only (tools/ablate.sh); all default off.
+#ifndef RT2_EXP_NO_BALLOT
+#define RT2_EXP_NO_BALLOT 0
+#endif
+#ifndef RT2_EXP_CHEAP_RNG
+#define RT2_EXP_CHEAP_RNG 0
+#endif
+#ifndef RT2_EXP_FAST_DIV
+#define RT2_EXP_FAST_DIV 0
+#endif
+#ifndef RT2_EXP_STAMPS
+#define RT2_EXP_STAMPS 0  // diagnostic build: per-section s_memtime sums into stats slots 9..12
+#endif
+#ifndef RT2_MIN_WAVES_PER_EU
+#define RT2_MIN_WAVES_PER_EU 1
+#endif
+
+extern __shared__ float4 s_dyn[];  // [lds_nodes scene records][stack_depth * kBlock stack words]
 
 struct f3 {
   float x, y, z;
@@ -59,59 +81,109 @@ __device__ __forceinline__ uint32_t bits(float f) { return __float_as_uint(f); }
 __device__ __forceinline__ float gmax(float x, float y) { return (x < y) ? y : x; }
 __device__ __forceinline__ float gmin(float x, float y) { return (y < x) ? y : x; }
 
-// ------------------------------------------------------------------------------------------
-// Philox4x32-10 path stream keyed by (seed, pixel, frame).
-struct Rng {
-  uint32_t k0, k1, a, b, block, idx;
-  uint32_t r0, r1, r2, r3;
-  __device__ __forceinline__ void init(uint32_t seed_lo, uint32_t seed_hi, uint32_t pixel, uint32_t frame) {
-    k0 = seed_lo;
-    k1 = seed_hi;
-    a = pixel;
-    b = frame;
-    block = 0;
-    idx = 4;
-  }
-  __device__ __forceinline__ void refill() {
-    uint32_t c0 = a, c1 = b, c2 = block++, c3 = kTagPathDev;
-    uint32_t key0 = k0, key1 = k1;
-#pragma unroll
-    for (int r = 0; r < 10; r++) {
-      uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
-      uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
-      uint32_t n0 = hi1 ^ c1 ^ key0, n2 = hi0 ^ c3 ^ key1;
-      c0 = n0;
-      c1 = lo1;
-      c2 = n2;
-      c3 = lo0;
-      key0 += 0x9E3779B9u;
-      key1 += 0xBB67AE85u;
+template <uint32_t F, uint32_t B>
+constexpr bool Has() {
+  return (F & B) != 0;
+}
+
+// Scene-record source: the LDS copy (kModeStackLds) or global memory. Loads go through a
+// __restrict__ parameter so wave-uniform indices (linear mode) become scalar loads.
+__device__ __forceinline__ float4 ldg4(const float4* __restrict__ p, uint32_t i) { return p[i]; }
+__device__ __forceinline__ uint32_t ldg1(const uint32_t* __restrict__ p, uint32_t i) { return p[i]; }
+
+template <int kMode>
+struct Nodes {
+  const float4* g;
+  __device__ __forceinline__ float4 operator[](uint32_t i) const {
+    if constexpr (kMode == kModeStackLds) {
+      return s_dyn[i];
+    } else {
+      return ldg4(g, i);
     }
-    r0 = c0;
-    r1 = c1;
-    r2 = c2;
-    r3 = c3;
-    idx = 0;
   }
-  __device__ __forceinline__ float uniform() {
-    if (idx == 4) refill();
-    uint32_t v = idx == 0 ? r0 : (idx == 1 ? r1 : (idx == 2 ? r2 : r3));
-    idx++;
-    return (float)(v >> 8) * (1.0f / 16777216.0f);
+  __device__ __forceinline__ uint32_t word(uint32_t rec, uint32_t k) const {  // 32-bit word k after record rec
+    if constexpr (kMode == kModeStackLds) {
+      return bits(reinterpret_cast<const float*>(s_dyn + rec)[k]);
+    } else {
+      return ldg1(reinterpret_cast<const uint32_t*>(g + rec), k);
+    }
   }
-  // Math.hpp:15 RandReal(min, max)
-  __device__ __forceinline__ float uniform(float mn, float mx) { return mn + uniform() * (mx - mn); }
-  static constexpr uint32_t kTagPathDev = 0x52543250u;
 };
 
-// Math.hpp:26-43
-__device__ __forceinline__ f3 rand_unit_vec3(Rng& g) {
+// ------------------------------------------------------------------------------------------
+// Philox4x32-10 path stream keyed by (seed, pixel, frame). Draws are taken in groups of K <= 4
+// consecutive values; `n` counts draws and the buffer holds the block of the last value drawn
+// ((n - 1) >> 2), so a group needs at most ONE Philox call (one refill site per call site instead
+// of one per value: under divergence every refill site executes for the whole wave).
+__device__ __forceinline__ void philox(uint32_t k0, uint32_t k1, uint32_t pixel, uint32_t frame, uint32_t block,
+                                       uint32_t& r0, uint32_t& r1, uint32_t& r2, uint32_t& r3) {
+  uint32_t c0 = pixel, c1 = frame, c2 = block, c3 = 0x52543250u, key0 = k0, key1 = k1;
+#pragma unroll
+  for (int r = 0; r < (RT2_EXP_CHEAP_RNG ? 2 : 10); r++) {
+    uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+    uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+    c0 = hi1 ^ c1 ^ key0;
+    c1 = lo1;
+    c2 = hi0 ^ c3 ^ key1;
+    c3 = lo0;
+    key0 += 0x9E3779B9u;
+    key1 += 0xBB67AE85u;
+  }
+  r0 = c0;
+  r1 = c1;
+  r2 = c2;
+  r3 = c3;
+}
+
+__device__ __forceinline__ uint32_t sel4(uint32_t i, uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3) {
+  return i == 0u ? r0 : (i == 1u ? r1 : (i == 2u ? r2 : r3));
+}
+__device__ __forceinline__ float to_unit(uint32_t v) { return (float)(v >> 8) * (1.0f / 16777216.0f); }
+
+// The per-lane path context the samplers need.
+struct Path {
+  uint32_t k0, k1, pix, frame;
+  uint32_t n;
+  uint32_t r0, r1, r2, r3;
+  __device__ __forceinline__ void start(uint32_t f) {
+    frame = f;
+    n = 0;  // buffer holds block -1: the first group refills
+  }
+  // K consecutive uniforms in [0,1) (24-bit mantissa), in stream order
+  template <int K>
+  __device__ __forceinline__ void take(float* out) {
+    uint32_t i = n & 3u;
+    bool fresh = i == 0u;
+    uint32_t v[K];
+#pragma unroll
+    for (int j = 0; j < K; j++) v[j] = sel4((i + (uint32_t)j) & 3u, r0, r1, r2, r3);
+    if (fresh || i + (uint32_t)K > 4u) {
+      philox(k0, k1, pix, frame, (n >> 2) + (fresh ? 0u : 1u), r0, r1, r2, r3);
+#pragma unroll
+      for (int j = 0; j < K; j++)
+        if (fresh || i + (uint32_t)j >= 4u) v[j] = sel4((i + (uint32_t)j) & 3u, r0, r1, r2, r3);
+    }
+    n += (uint32_t)K;
+#pragma unroll
+    for (int j = 0; j < K; j++) out[j] = to_unit(v[j]);
+  }
+  __device__ __forceinline__ float uniform() {
+    float u[1];
+    take<1>(u);
+    return u[0];
+  }
+};
+
+// Math.hpp:15 RandReal(min, max) = min + RandReal() * (max - min)
+__device__ __forceinline__ float rand_range(float u, float mn, float mx) { return mn + u * (mx - mn); }
+
+// Math.hpp:26-43: RandUnitVec3 = normalize(RandInUnitSphere()), one refill site per attempt
+__device__ __forceinline__ f3 rand_unit_vec3(Path& g) {
   f3 p;
   while (true) {
-    float x = g.uniform(-1.0f, 1.0f);
-    float y = g.uniform(-1.0f, 1.0f);
-    float z = g.uniform(-1.0f, 1.0f);
-    p = mk(x, y, z);
+    float u[3];
+    g.take<3>(u);
+    p = mk(rand_range(u[0], -1.0f, 1.0f), rand_range(u[1], -1.0f, 1.0f), rand_range(u[2], -1.0f, 1.0f));
     float lsq = dot(p, p);
     if (lsq > 0.0f && lsq <= 1.0f) break;  // 1e-160 < |p|^2 <= 1 for a float |p|^2
   }
@@ -129,19 +201,12 @@ __device__ __forceinline__ f3 refract(f3 uv, f3 n, float etai_over_etat) {
   return perp + par;
 }
 
-struct Hit {
-  float t;
-  f3 p, n;
-  uint32_t mat;
-  bool front;
-};
-
 struct Counters {
   uint32_t bvh, quad, sphere, xform, medium, list;
 };
 
 // ------------------------------------------------------------------------------------------
-// Primitive tests. Each returns true and fills (t, p, n, front, mat) in the ray's space.
+// Primitive tests: return whether the primitive is hit inside the interval and its t.
 
 // AABB::Hit (AABB.hpp:34-47); inv = 1/d per axis (the same value the reference computes per node)
 __device__ __forceinline__ bool aabb_hit(float4 lo, float4 hi, f3 o, f3 inv, float tmin, float tmax) {
@@ -165,12 +230,18 @@ __device__ __forceinline__ bool aabb_hit(float4 lo, float4 hi, f3 o, f3 inv, flo
 }
 
 // Quad::Hit (Quad.cpp:19-43): inclusive interval (Contains)
-__device__ __forceinline__ bool quad_hit(const float4* N, uint32_t off, f3 o, f3 d, float tmin, float tmax, Hit& h) {
+template <int kMode>
+__device__ __forceinline__ bool quad_t(const Nodes<kMode>& N, uint32_t off, f3 o, f3 d, float tmin, float tmax,
+                                       float& t_out) {
   float4 r0 = N[off];
   f3 n = xyz(r0);
   float n_dot = dot(n, d);
-  if (fabsf(n_dot) <= 1e-8f) return false;
+  if (fabsf(n_dot) <= 1e-8f) return false;  // |n.d| < 1e-8 (double)
+#if RT2_EXP_FAST_DIV
+  float t = __fdividef(r0.w - dot(n, o), n_dot);
+#else
   float t = (r0.w - dot(n, o)) / n_dot;
+#endif
   if (!(tmin <= t && t <= tmax)) return false;
   float4 r1 = N[off + 1], r2 = N[off + 2], r3 = N[off + 3], r4 = N[off + 4];
   f3 p = o + d * t;
@@ -178,17 +249,14 @@ __device__ __forceinline__ bool quad_hit(const float4* N, uint32_t off, f3 o, f3
   float alpha = dot(xyz(r4), cross(pv, xyz(r3)));
   float beta = dot(xyz(r4), cross(xyz(r2), pv));
   if (!(0.0f <= alpha && alpha <= 1.0f) || !(0.0f <= beta && beta <= 1.0f)) return false;
-  h.t = t;
-  h.p = p;
-  h.mat = bits(r1.w);
-  h.front = dot(d, n) < 0.0f;
-  h.n = h.front ? n : -n;
+  t_out = t;
   return true;
 }
 
 // Sphere::Hit (Sphere.cpp:7-37): exclusive interval (Surrounds); uv is dead output
-__device__ __forceinline__ bool sphere_hit(const float4* N, uint32_t off, f3 o, f3 d, float time, float tmin,
-                                           float tmax, Hit& h) {
+template <int kMode>
+__device__ __forceinline__ bool sphere_t(const Nodes<kMode>& N, uint32_t off, f3 o, f3 d, float time, float tmin,
+                                         float tmax, float& t_out) {
   float4 r0 = N[off], r1 = N[off + 1];
   f3 center = xyz(r0) + xyz(r1) * time;
   f3 oc = center - o;
@@ -203,57 +271,64 @@ __device__ __forceinline__ bool sphere_hit(const float4* N, uint32_t off, f3 o, 
     root = (hh + sq) / a;
     if (!(tmin < root && root < tmax)) return false;
   }
-  h.t = root;
-  h.p = o + d * root;
-  h.mat = bits(r1.w);
-  f3 outward = (h.p - center) / r0.w;
-  h.front = dot(d, outward) < 0.0f;
-  h.n = h.front ? outward : -outward;
+  t_out = root;
   return true;
 }
 
-// Closest t of a ConstantMedium boundary (quad, sphere or a list of them) on [lo, hi]
-__device__ __forceinline__ bool boundary_hit(const float4* N, uint32_t ref, f3 o, f3 d, float time, float lo,
-                                             float hi, float& t_out, Counters& cnt) {
-  uint32_t kind = ref >> 28, off = ref & kOffsetMask;
-  Hit tmp;
-  if (kind == kQuad) {
-    cnt.quad++;
-    if (!quad_hit(N, off, o, d, lo, hi, tmp)) return false;
-    t_out = tmp.t;
-    return true;
+// Quad::Hit split in two: the candidate (pure function of the ray) and the interval test. The
+// reference tests the interval before the interior; both are side-effect free, so testing the
+// interior first and applying the interval afterwards gives the same hit.
+template <int kMode>
+__device__ __forceinline__ bool quad_cand(const Nodes<kMode>& N, uint32_t off, f3 o, f3 d, float& t_out) {
+  float4 r0 = N[off];
+  f3 n = xyz(r0);
+  float n_dot = dot(n, d);
+  float t = (r0.w - dot(n, o)) / n_dot;
+  float4 r1 = N[off + 1], r2 = N[off + 2], r3 = N[off + 3], r4 = N[off + 4];
+  f3 p = o + d * t;
+  f3 pv = p - xyz(r1);
+  float alpha = dot(xyz(r4), cross(pv, xyz(r3)));
+  float beta = dot(xyz(r4), cross(xyz(r2), pv));
+  t_out = t;
+  return !(fabsf(n_dot) <= 1e-8f) && (0.0f <= alpha && alpha <= 1.0f) && (0.0f <= beta && beta <= 1.0f);
+}
+
+template <uint32_t F, int kMode>
+__device__ __forceinline__ bool prim_t(const Nodes<kMode>& N, uint32_t ref, f3 o, f3 d, float time, float tmin,
+                                       float tmax, float& t, Counters& cnt) {
+  uint32_t off = ref & kOffsetMask;
+  if constexpr (Has<F, kFeatSphere>()) {
+    if ((ref >> 28) == kSphere) {
+      cnt.sphere++;
+      return sphere_t(N, off, o, d, time, tmin, tmax, t);
+    }
   }
-  if (kind == kSphere) {
-    cnt.sphere++;
-    if (!sphere_hit(N, off, o, d, time, lo, hi, tmp)) return false;
-    t_out = tmp.t;
-    return true;
-  }
-  // leaf-only list (box): sequential, shrinking max
-  uint32_t n = bits(N[off].x);
+  cnt.quad++;
+  return quad_t(N, off, o, d, tmin, tmax, t);
+}
+
+// Closest t of a ConstantMedium boundary (quad, sphere or a leaf-only list) on [lo, hi]
+template <uint32_t F, int kMode>
+__device__ __forceinline__ bool boundary_t(const Nodes<kMode>& N, uint32_t ref, f3 o, f3 d, float time, float lo,
+                                           float hi, float& t_out, Counters& cnt) {
+  if ((ref >> 28) != kList) return prim_t<F>(N, ref, o, d, time, lo, hi, t_out, cnt);
+  uint32_t off = ref & kOffsetMask;
+  uint32_t n = N.word(off, 0);
   bool any = false;
   for (uint32_t k = 0; k < n; k++) {
-    uint32_t c = bits(reinterpret_cast<const float*>(N + off + 1)[k]);
-    uint32_t ck = c >> 28, co = c & kOffsetMask;
-    bool hit;
-    if (ck == kQuad) {
-      cnt.quad++;
-      hit = quad_hit(N, co, o, d, lo, hi, tmp);
-    } else {
-      cnt.sphere++;
-      hit = sphere_hit(N, co, o, d, time, lo, hi, tmp);
-    }
-    if (hit) {
+    float t;
+    if (prim_t<F>(N, N.word(off + 1, k), o, d, time, lo, hi, t, cnt)) {
       any = true;
-      hi = tmp.t;
+      hi = t;
     }
   }
   if (any) t_out = hi;
   return any;
 }
 
-// World -> model space of one XFORM (Transform.cpp:13-20)
-__device__ __forceinline__ void to_model(const float4* N, uint32_t off, f3& o, f3& d) {
+// Parent space -> model space of one XFORM (Transform.cpp:13-20)
+template <int kMode>
+__device__ __forceinline__ void to_model(const Nodes<kMode>& N, uint32_t off, f3& o, f3& d) {
   float4 c0 = N[off], c1 = N[off + 1], c2 = N[off + 2], c3 = N[off + 3];
   f3 no = mk((c0.x * o.x + c1.x * o.y) + (c2.x * o.z + c3.x), (c0.y * o.x + c1.y * o.y) + (c2.y * o.z + c3.y),
              (c0.z * o.x + c1.z * o.y) + (c2.z * o.z + c3.z));
@@ -263,156 +338,298 @@ __device__ __forceinline__ void to_model(const float4* N, uint32_t off, f3& o, f
   d = normalize(nd);
 }
 
-// Ray in the space of XFORM `xref` (kRefNone = world), rebuilt from the world ray through the
-// chain of enclosing transforms (only needed for nested transforms; depth <= 8).
-__device__ void ray_in_space(const float4* N, uint32_t xref, f3 wo, f3 wd, f3& o, f3& d) {
+// Ray in the space of XFORM `xref` (kRefNone = world), rebuilt from the world ray through the chain
+// of enclosing transforms; recomputing gives the same bits as the traversal's incremental path.
+template <int kMode>
+__device__ __forceinline__ void ray_in_space(const Nodes<kMode>& N, uint32_t xref, f3 wo, f3 wd, f3& o, f3& d) {
   o = wo;
   d = wd;
   if (xref == kRefNone) return;
+  uint32_t parent = N.word((xref & kOffsetMask) + 1, 3);
+  if (parent == kRefNone) {  // the common single-level case
+    to_model(N, xref & kOffsetMask, o, d);
+    return;
+  }
   uint32_t chain[8];
   int n = 0;
-  for (uint32_t x = xref; x != kRefNone && n < 8; x = bits(N[(x & kOffsetMask) + 1].w)) chain[n++] = x;
+  for (uint32_t x = xref; x != kRefNone && n < 8; x = N.word((x & kOffsetMask) + 1, 3)) chain[n++] = x;
   for (int k = n - 1; k >= 0; k--) to_model(N, chain[k] & kOffsetMask, o, d);
 }
+
+// ConstantMedium::Hit (ConstantMedium.cpp:14-58) on [tmin, tmax]: two boundary queries, then one
+// random number for the free-flight distance. Returns the medium's t.
+template <uint32_t F, int kMode>
+__device__ __forceinline__ bool medium_t(const Nodes<kMode>& N, uint32_t off, f3 o, f3 d, float time, float tmin,
+                                         float tmax, Path& path, float& t_out, Counters& cnt) {
+  float4 r0 = N[off];
+  uint32_t bref = bits(r0.z);
+  float t1, t2;
+  if (!boundary_t<F>(N, bref, o, d, time, -FLT_MAX, FLT_MAX, t1, cnt)) return false;
+  if (!boundary_t<F>(N, bref, o, d, time, (float)((double)t1 + 0.0001), FLT_MAX, t2, cnt)) return false;
+  t1 = fmaxf(t1, tmin);
+  t2 = fminf(t2, tmax);
+  if (t1 >= t2) return false;
+  t1 = fmaxf(t1, 0.0f);
+  float len = sqrtf(dot(d, d));
+  float inside = (t2 - t1) * len;
+  float hit_dist = r0.x * (float)log((double)path.uniform());
+  if (hit_dist > inside) return false;
+  t_out = t1 + hit_dist / len;
+  return true;
+}
+
+struct HitRef {
+  float t;
+  uint32_t prim;  // ref of the quad / sphere / medium that produced the closest hit
+  uint32_t xf;    // innermost enclosing transform of that primitive (kRefNone = world)
+};
 
 // ------------------------------------------------------------------------------------------
 // Closest hit over the scene program (HittableList{BVHNode} at the root, App.cpp:126).
 // Reference semantics preserved: left-then-right, right subtree pruned by the current closest t,
 // model-space t of transformed children compared as-is (Transform.cpp:82), span-1 media tested
 // twice with fresh random numbers, media boundaries queried on (-FLT_MAX, FLT_MAX).
-template <bool kStats>
-__device__ bool trace(const RenderParams& P, f3 wo, f3 wd, float time, Rng& rng, Hit& h, uint32_t* stk,
-                      Counters& cnt, bool& overflow) {
-  const float4* N = reinterpret_cast<const float4*>(P.nodes);
+
+// Stack traversal (any scene): each lane walks its own steps — LDS stack pops, or the next child of
+// a leaf list through a per-lane cursor — one step per loop trip.
+template <uint32_t F, int kMode, bool kStats>
+__device__ __forceinline__ bool trace_stack(const RenderParams& P, const Nodes<kMode>& N, f3 wo, f3 wd, float time,
+                                            Path& path, HitRef& h, uint32_t* stk, Counters& cnt, bool& overflow) {
   f3 o = wo, d = wd;
-  f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+  const f3 winv = mk(1.0f / wd.x, 1.0f / wd.y, 1.0f / wd.z);
+  f3 inv = winv;
   const float tmin = 0.001f;  // Interval{0.001, kInfinity}
   float tmax = FLT_MAX;
   bool any = false;
-  int depth = 0;           // transform nesting depth
-  uint32_t hitmask = 0;    // bit k: a hit was recorded inside the transform at depth k
+  uint32_t cur_xf = kRefNone;
+  const int cap = P.stack_depth;
   int sp = 0;
-  stk[0] = P.root;
-  sp = 1;
-  while (sp > 0) {
-    sp--;
-    uint32_t ref = stk[sp * kBlock];
-    uint32_t kind = ref >> 28, off = ref & kOffsetMask;
-    if (kind == kBvh) {
+  uint32_t lword = 0, lrem = 0;  // leaf-list cursor: next child-ref word, children left
+  uint32_t cur = P.root;         // next step
+  while (cur != kRefNone) {
+    uint32_t kind = cur >> 28, off = cur & kOffsetMask;
+    if (kind == kQuad || (Has<F, kFeatSphere>() && kind == kSphere)) {
+      float t;
+      if (prim_t<F>(N, cur, o, d, time, tmin, tmax, t, cnt)) {
+        tmax = t;
+        any = true;
+        h.prim = cur;
+        h.xf = cur_xf;
+      }
+    } else if (kind == kBvh) {
       if (kStats) cnt.bvh++;
       float4 lo = N[off], hi = N[off + 1];
       if (aabb_hit(lo, hi, o, inv, tmin, tmax)) {
         uint32_t right = bits(hi.w);
-        if (sp + 2 > kTraversalStack) {
-          overflow = true;
-          continue;
+        if (right != kRefNone) {
+          if (sp + 1 > cap) {
+            overflow = true;
+          } else {
+            stk[(sp++) * kBlock] = right;
+          }
         }
-        if (right != kRefNone) stk[(sp++) * kBlock] = right;
-        stk[(sp++) * kBlock] = bits(lo.w);
-      }
-    } else if (kind == kQuad) {
-      if (kStats) cnt.quad++;
-      if (quad_hit(N, off, o, d, tmin, tmax, h)) {
-        tmax = h.t;
-        any = true;
-        hitmask |= 1u << depth;
-      }
-    } else if (kind == kSphere) {
-      if (kStats) cnt.sphere++;
-      if (sphere_hit(N, off, o, d, time, tmin, tmax, h)) {
-        tmax = h.t;
-        any = true;
-        hitmask |= 1u << depth;
+        cur = bits(lo.w);
+        continue;  // the left child is the next step (no stack round trip)
       }
     } else if (kind == kList) {
       if (kStats) cnt.list++;
-      float4 hdr = N[off];
-      uint32_t n = bits(hdr.x);
-      const float* refs = reinterpret_cast<const float*>(N + off + 1);
-      if (bits(hdr.y) & kListLeafOnly) {
-        for (uint32_t k = 0; k < n; k++) {
-          uint32_t c = bits(refs[k]);
-          uint32_t co = c & kOffsetMask;
-          bool hit;
-          if ((c >> 28) == kQuad) {
-            if (kStats) cnt.quad++;
-            hit = quad_hit(N, co, o, d, tmin, tmax, h);
-          } else {
-            if (kStats) cnt.sphere++;
-            hit = sphere_hit(N, co, o, d, time, tmin, tmax, h);
-          }
-          if (hit) {
-            tmax = h.t;
-            any = true;
-            hitmask |= 1u << depth;
-          }
-        }
-      } else {
-        if (sp + (int)n > kTraversalStack) {
-          overflow = true;
-          continue;
-        }
-        for (int k = (int)n - 1; k >= 0; k--) stk[(sp++) * kBlock] = bits(refs[k]);
-      }
-    } else if (kind == kXform) {
-      if (kStats) cnt.xform++;
-      if (sp + 2 > kTraversalStack || depth >= 31) {
+      uint32_t n = N.word(off, 0);
+      bool leaf_only = true;
+      if constexpr (Has<F, kFeatGenList>()) leaf_only = (N.word(off, 1) & kListLeafOnly) != 0u;
+      if (leaf_only) {
+        lword = 4u * (off + 1u);
+        lrem = n;
+      } else if (sp + (int)n > cap) {
         overflow = true;
+      } else {
+        for (int k = (int)n - 1; k >= 0; k--) stk[(sp++) * kBlock] = N.word(off + 1, (uint32_t)k);
+      }
+    } else if (Has<F, kFeatXform>() && kind == kXform) {
+      if (kStats) cnt.xform++;
+      if (sp + 1 > cap) {
+        overflow = true;
+      } else {
+        to_model(N, off, o, d);
+        inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+        cur_xf = cur;
+        stk[(sp++) * kBlock] = make_ref(kXformExit, off);
+        cur = N.word(off, 3);  // the transformed child is the next step
         continue;
       }
-      depth++;
-      hitmask &= ~(1u << depth);
-      to_model(N, off, o, d);
-      inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-      stk[(sp++) * kBlock] = make_ref(kXformExit, off);
-      stk[(sp++) * kBlock] = bits(N[off].w);
-    } else if (kind == kXformExit) {
-      if ((hitmask >> depth) & 1u) {
-        // back to the parent space: point via M, normal via transpose(inverse(M)) (Transform.cpp:85-86)
-        float4 m0 = N[off + 4], m1 = N[off + 5], m2 = N[off + 6], m3 = N[off + 7];
-        f3 p = h.p;
-        h.p = mk((m0.x * p.x + m1.x * p.y) + (m2.x * p.z + m3.x), (m0.y * p.x + m1.y * p.y) + (m2.y * p.z + m3.y),
-                 (m0.z * p.x + m1.z * p.y) + (m2.z * p.z + m3.z));
-        float4 c0 = N[off], c1 = N[off + 1], c2 = N[off + 2];
-        f3 n = h.n;
-        h.n = normalize(mk(c0.x * n.x + c0.y * n.y + c0.z * n.z, c1.x * n.x + c1.y * n.y + c1.z * n.z,
-                           c2.x * n.x + c2.y * n.y + c2.z * n.z));
-        hitmask |= 1u << (depth - 1);
+    } else if (Has<F, kFeatXform>() && kind == kXformExit) {
+      cur_xf = N.word(off + 1, 3);  // parent transform
+      if (cur_xf == kRefNone) {
+        o = wo;
+        d = wd;
+        inv = winv;
+      } else {
+        ray_in_space(N, cur_xf, wo, wd, o, d);
+        inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
       }
-      depth--;
-      ray_in_space(N, bits(N[off + 1].w), wo, wd, o, d);
-      inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    } else {  // kMedium
+    } else if (Has<F, kFeatMedium>() && kind == kMedium) {
       if (kStats) cnt.medium++;
-      float4 r0 = N[off];
-      uint32_t bref = bits(r0.z);
-      float t1, t2;
-      if (!boundary_hit(N, bref, o, d, time, -FLT_MAX, FLT_MAX, t1, cnt)) continue;
-      if (!boundary_hit(N, bref, o, d, time, (float)((double)t1 + 0.0001), FLT_MAX, t2, cnt)) continue;
-      t1 = fmaxf(t1, tmin);
-      t2 = fminf(t2, tmax);
-      if (t1 >= t2) continue;
-      t1 = fmaxf(t1, 0.0f);
-      float len = sqrtf(dot(d, d));
-      float inside = (t2 - t1) * len;
-      float hit_dist = r0.x * (float)log((double)rng.uniform());
-      if (hit_dist > inside) continue;
-      h.t = t1 + hit_dist / len;
-      h.p = o + d * h.t;
-      h.n = mk(1.0f, 0.0f, 0.0f);
-      h.front = true;
-      h.mat = bits(r0.y);
-      tmax = h.t;
-      any = true;
-      hitmask |= 1u << depth;
+      float t;
+      if (medium_t<F>(N, off, o, d, time, tmin, tmax, path, t, cnt)) {
+        tmax = t;
+        any = true;
+        h.prim = cur;
+        h.xf = cur_xf;
+      }
+    }
+    // next step: the leaf-list cursor first, then the stack
+    if (lrem != 0u) {
+      cur = N.word(0, lword++);
+      lrem--;
+    } else if (sp > 0) {
+      cur = stk[(--sp) * kBlock];
+    } else {
+      cur = kRefNone;
     }
   }
+  h.t = tmax;
   return any;
+}
+
+// Threaded traversal (small scenes): all lanes of the wave walk the pre-order program P.lin in
+// lockstep. Each lane keeps the index of its next step; the wave executes the smallest pending
+// index, so the step kind is wave-uniform (no divergence between kinds) and the step's records are
+// scalar loads. A lane whose AABB test misses jumps to the node's skip index. Per lane the visit
+// order is exactly the stack traversal's.
+template <uint32_t F, bool kStats>
+__device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd, float time, Path& path, HitRef& h,
+                                             Counters& cnt) {
+  const Nodes<kModeLinear> N{reinterpret_cast<const float4*>(P.nodes)};
+  const uint4* __restrict__ prog = reinterpret_cast<const uint4*>(P.lin);
+  f3 o = wo, d = wd;
+  const f3 winv = mk(1.0f / wd.x, 1.0f / wd.y, 1.0f / wd.z);
+  f3 inv = winv;
+  const float tmin = 0.001f;
+  float tmax = FLT_MAX;
+  bool any = false;
+  uint32_t cur_xf = kRefNone;
+  uint32_t next = 0;  // this lane's next step
+  const uint32_t len = P.lin_len;
+  while (true) {
+    // wave-uniform step = min over live lanes of `next`
+    uint32_t i = __builtin_amdgcn_readfirstlane(next);
+    unsigned long long lower;
+    while ((lower = __ballot(next < i)) != 0ull) i = __builtin_amdgcn_readlane(next, __ffsll((long long)lower) - 1);
+    if (i >= len) break;
+    const uint4 st = prog[i];
+    const uint32_t kind = st.x, off = st.z;
+    if (next != i) continue;
+    next = i + 1u;
+    if (kind == kBvh) {
+      if (kStats) cnt.bvh++;
+      if (!aabb_hit(N[off], N[off + 1], o, inv, tmin, tmax)) next = st.y;
+    } else if (kind == kQuad) {
+      // a run of st.w quads: two candidate computations in flight, applied in program order
+      const uint32_t run = st.w;
+      for (uint32_t k = 0; k < run; k += 2) {
+        const uint32_t off0 = prog[i + k].z;
+        const bool two = k + 1 < run;
+        const uint32_t off1 = two ? prog[i + k + 1].z : off0;
+        float t0, t1;
+        bool ok0 = quad_cand(N, off0, o, d, t0);
+        bool ok1 = quad_cand(N, off1, o, d, t1) && two;
+        if (kStats) cnt.quad += two ? 2 : 1;
+        if (ok0 && tmin <= t0 && t0 <= tmax) {
+          tmax = t0;
+          any = true;
+          h.prim = make_ref(kQuad, off0);
+          h.xf = cur_xf;
+        }
+        if (ok1 && tmin <= t1 && t1 <= tmax) {
+          tmax = t1;
+          any = true;
+          h.prim = make_ref(kQuad, off1);
+          h.xf = cur_xf;
+        }
+      }
+      next = i + run;
+    } else if (Has<F, kFeatSphere>() && kind == kSphere) {
+      float t;
+      uint32_t ref = make_ref(kind, off);
+      if (prim_t<F>(N, ref, o, d, time, tmin, tmax, t, cnt)) {
+        tmax = t;
+        any = true;
+        h.prim = ref;
+        h.xf = cur_xf;
+      }
+    } else if (Has<F, kFeatXform>() && kind == kXform) {
+      if (kStats) cnt.xform++;
+      to_model(N, off, o, d);
+      inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+      cur_xf = make_ref(kXform, off);
+    } else if (Has<F, kFeatXform>() && kind == kXformExit) {
+      cur_xf = st.w;
+      if (cur_xf == kRefNone) {
+        o = wo;
+        d = wd;
+        inv = winv;
+      } else {
+        ray_in_space(N, cur_xf, wo, wd, o, d);
+        inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+      }
+    } else if (Has<F, kFeatMedium>() && kind == kMedium) {
+      if (kStats) cnt.medium++;
+      float t;
+      if (medium_t<F>(N, off, o, d, time, tmin, tmax, path, t, cnt)) {
+        tmax = t;
+        any = true;
+        h.prim = make_ref(kMedium, off);
+        h.xf = cur_xf;
+      }
+    }
+  }
+  h.t = tmax;
+  return any;
+}
+
+// The closest hit's record in world space (what the reference's rec holds after the chain of
+// TransformedHittable::Hit returns): point, normal, front_face, material.
+template <uint32_t F, int kMode>
+__device__ __forceinline__ void resolve_hit(const Nodes<kMode>& N, const HitRef& h, f3 wo, f3 wd, float time, f3& p,
+                                            f3& n, bool& front, uint32_t& mat) {
+  f3 o = wo, d = wd;
+  if constexpr (Has<F, kFeatXform>()) ray_in_space(N, h.xf, wo, wd, o, d);
+  uint32_t kind = h.prim >> 28, off = h.prim & kOffsetMask;
+  p = o + d * h.t;
+  if (Has<F, kFeatMedium>() && kind == kMedium) {
+    n = mk(1.0f, 0.0f, 0.0f);
+    front = true;
+    mat = N.word(off, 1);
+  } else if (Has<F, kFeatSphere>() && kind == kSphere) {
+    float4 r0 = N[off], r1 = N[off + 1];
+    f3 center = xyz(r0) + xyz(r1) * time;
+    f3 outward = (p - center) / r0.w;
+    front = dot(d, outward) < 0.0f;
+    n = front ? outward : -outward;
+    mat = bits(r1.w);
+  } else {
+    f3 qn = xyz(N[off]);
+    front = dot(d, qn) < 0.0f;
+    n = front ? qn : -qn;
+    mat = N.word(off + 1, 3);
+  }
+  if constexpr (Has<F, kFeatXform>()) {
+    // back through every enclosing transform, innermost first (Transform.cpp:85-86)
+    for (uint32_t x = h.xf; x != kRefNone;) {
+      uint32_t xo = x & kOffsetMask;
+      float4 m0 = N[xo + 4], m1 = N[xo + 5], m2 = N[xo + 6], m3 = N[xo + 7];
+      p = mk((m0.x * p.x + m1.x * p.y) + (m2.x * p.z + m3.x), (m0.y * p.x + m1.y * p.y) + (m2.y * p.z + m3.y),
+             (m0.z * p.x + m1.z * p.y) + (m2.z * p.z + m3.z));
+      float4 c0 = N[xo], c1 = N[xo + 1], c2 = N[xo + 2];
+      n = normalize(mk(c0.x * n.x + c0.y * n.y + c0.z * n.z, c1.x * n.x + c1.y * n.y + c1.z * n.z,
+                       c2.x * n.x + c2.y * n.y + c2.z * n.z));
+      x = bits(c1.w);
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------------
 // Textures (Texture.cpp:7-22, PerlinNoiseGen.cpp:10-88)
-__device__ float perlin_noise(const RenderParams& P, uint32_t voff, uint32_t poff, uint32_t pc, f3 p) {
+__device__ __forceinline__ float perlin_noise(const RenderParams& P, uint32_t voff, uint32_t poff, uint32_t pc, f3 p) {
   const float4* V = reinterpret_cast<const float4*>(P.perlin_vec) + voff;
   const int* Px = P.perlin_perm + poff;
   const int* Py = Px + pc;
@@ -424,11 +641,8 @@ __device__ float perlin_noise(const RenderParams& P, uint32_t voff, uint32_t pof
   float vv = v * v * (3.0f - 2.0f * v);
   float ww = w * w * (3.0f - 2.0f * w);
   float accum = 0.0f;
-#pragma unroll
   for (int di = 0; di < 2; di++)
-#pragma unroll
     for (int dj = 0; dj < 2; dj++)
-#pragma unroll
       for (int dk = 0; dk < 2; dk++) {
         int idx = Px[(i + di) & 255] ^ Py[(j + dj) & 255] ^ Pz[(k + dk) & 255];
         f3 g = xyz(V[idx]);
@@ -441,67 +655,93 @@ __device__ float perlin_noise(const RenderParams& P, uint32_t voff, uint32_t pof
   return accum;
 }
 
-__device__ f3 tex_value(const RenderParams& P, uint32_t idx, f3 p) {
+template <uint32_t F>
+__device__ __forceinline__ f3 tex_value(const RenderParams& P, uint32_t idx, f3 p) {
   const float4* T = reinterpret_cast<const float4*>(P.textures);
   for (int guard = 0; guard < 32; guard++) {
-    float4 t0 = T[3 * idx], t1 = T[3 * idx + 1];
+    float4 t0 = T[3 * idx];
     uint32_t type = bits(t0.x);
-    if (type == kTexSolid) return mk(t0.y, t0.z, t0.w);
-    if (type == kTexChecker) {
-      f3 sp = t1.x * p;
-      int ix = (int)floorf(sp.x), iy = (int)floorf(sp.y), iz = (int)floorf(sp.z);
-      idx = ((ix + iy + iz) % 2 == 0) ? bits(t1.y) : bits(t1.z);
-      continue;
-    }
-    float4 t2 = T[3 * idx + 2];
-    uint32_t voff = bits(t2.x), poff = bits(t2.y), pc = bits(t2.z);
-    f3 alb = mk(t0.y, t0.z, t0.w) * 0.5f;
-    if (bits(t1.w) == 1u) {  // NoiseType::kMarble
-      float acc = 0.0f, weight = 1.0f;
-      f3 tp = p;
-      for (int k = 0; k < 7; k++) {
-        acc += weight * perlin_noise(P, voff, poff, pc, tp);
-        weight *= 0.5f;
-        tp = tp * 2.0f;
+    if (!(Has<F, kFeatChecker>() || Has<F, kFeatNoise>()) || type == kTexSolid) return mk(t0.y, t0.z, t0.w);
+    float4 t1 = T[3 * idx + 1];
+    if constexpr (Has<F, kFeatChecker>()) {
+      if (type == kTexChecker) {
+        f3 sp = t1.x * p;
+        int ix = (int)floorf(sp.x), iy = (int)floorf(sp.y), iz = (int)floorf(sp.z);
+        idx = ((ix + iy + iz) % 2 == 0) ? bits(t1.y) : bits(t1.z);
+        continue;
       }
-      float arg = t1.x * p.z + 10.0f * fabsf(acc);
-      return alb * (1.0f + (float)sin((double)arg));
     }
-    return alb * (1.0f + perlin_noise(P, voff, poff, pc, t1.x * p));
+    if constexpr (Has<F, kFeatNoise>()) {
+      float4 t2 = T[3 * idx + 2];
+      uint32_t voff = bits(t2.x), poff = bits(t2.y), pc = bits(t2.z);
+      f3 alb = mk(t0.y, t0.z, t0.w) * 0.5f;
+      if (bits(t1.w) == 1u) {  // NoiseType::kMarble: turbulence, 7 octaves
+        float acc = 0.0f, weight = 1.0f;
+        f3 tp = p;
+        for (int k = 0; k < 7; k++) {
+          acc += weight * perlin_noise(P, voff, poff, pc, tp);
+          weight *= 0.5f;
+          tp = tp * 2.0f;
+        }
+        float arg = t1.x * p.z + 10.0f * fabsf(acc);
+        return alb * (1.0f + (float)sin((double)arg));
+      }
+      return alb * (1.0f + perlin_noise(P, voff, poff, pc, t1.x * p));
+    }
+    break;
   }
   return mk(0.0f, 0.0f, 0.0f);  // checker cycle (the reference recurses forever)
 }
 
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ void camera_ray(const RenderParams& P, int x, int y, int s_i, int s_j, Rng& g, f3& o,
-                                           f3& d, float& time) {
+template <uint32_t F>
+__device__ __forceinline__ void camera_ray(const RenderParams& P, int s_i, int s_j, Path& g, f3& o, f3& d,
+                                           float& time) {
   const CameraParams& C = P.cam;
-  float px = ((float)s_i + g.uniform()) * C.recip_sqrt_spp - 0.5f;
-  float py = ((float)s_j + g.uniform()) * C.recip_sqrt_spp - 0.5f;
+  int x = (int)(g.pix % (uint32_t)P.width), y = (int)(g.pix / (uint32_t)P.width);
+  float u[3];
+  bool defocus = Has<F, kFeatDefocus>() && !(C.defocus_angle <= 0.0f);
+  if (defocus) {
+    g.take<2>(u);
+  } else {
+    g.take<3>(u);  // px, py, time
+  }
+  float px = ((float)s_i + u[0]) * C.recip_sqrt_spp - 0.5f;
+  float py = ((float)s_j + u[1]) * C.recip_sqrt_spp - 0.5f;
   f3 p00 = mk(C.pixel00[0], C.pixel00[1], C.pixel00[2]);
   f3 du = mk(C.du[0], C.du[1], C.du[2]);
   f3 dv = mk(C.dv[0], C.dv[1], C.dv[2]);
   f3 pc = (p00 + (((float)x + px) * du)) + (((float)y + py) * dv);
   f3 c = mk(C.center[0], C.center[1], C.center[2]);
-  if (!(C.defocus_angle <= 0.0f)) {
-    float dx, dy;
-    while (true) {  // RandInUnitDisk (x drawn before y)
-      dx = g.uniform(-1.0f, 1.0f);
-      dy = g.uniform(-1.0f, 1.0f);
-      if ((dx * dx + dy * dy) + 0.0f * 0.0f < 1.0f) break;
+  if constexpr (Has<F, kFeatDefocus>()) {
+    if (defocus) {
+      float dx, dy;
+      while (true) {  // RandInUnitDisk (x drawn before y)
+        float w[2];
+        g.take<2>(w);
+        dx = rand_range(w[0], -1.0f, 1.0f);
+        dy = rand_range(w[1], -1.0f, 1.0f);
+        if ((dx * dx + dy * dy) + 0.0f * 0.0f < 1.0f) break;
+      }
+      c = (c + (dx * mk(C.defocus_u[0], C.defocus_u[1], C.defocus_u[2]))) +
+          (dy * mk(C.defocus_v[0], C.defocus_v[1], C.defocus_v[2]));
+      u[2] = g.uniform();
     }
-    c = (c + (dx * mk(C.defocus_u[0], C.defocus_u[1], C.defocus_u[2]))) +
-        (dy * mk(C.defocus_v[0], C.defocus_v[1], C.defocus_v[2]));
   }
-  time = g.uniform();
+  time = u[2];
   o = c;
   d = normalize(pc - c);
 }
 
-template <bool kStats>
-__global__ __launch_bounds__(kBlock) void render_kernel(const RenderParams P) {
-  __shared__ uint32_t s_stack[kTraversalStack * kBlock];
-  uint32_t* stk = s_stack + threadIdx.x;
+template <uint32_t F, int kMode, bool kStats>
+__global__ __launch_bounds__(kBlock, RT2_MIN_WAVES_PER_EU) void render_kernel(const RenderParams P) {
+  Nodes<kMode> N{reinterpret_cast<const float4*>(P.nodes)};
+  if constexpr (kMode == kModeStackLds) {
+    const float4* src = reinterpret_cast<const float4*>(P.nodes);
+    for (uint32_t i = threadIdx.x; i < P.lds_nodes; i += kBlock) s_dyn[i] = src[i];
+    __syncthreads();
+  }
+  uint32_t* stk = reinterpret_cast<uint32_t*>(s_dyn + (kMode == kModeStackLds ? P.lds_nodes : 0u)) + threadIdx.x;
   const int lane = (int)__lane_id();
   const float4* M = reinterpret_cast<const float4*>(P.materials);
   const f3 bg = mk(P.background[0], P.background[1], P.background[2]);
@@ -509,22 +749,39 @@ __global__ __launch_bounds__(kBlock) void render_kernel(const RenderParams P) {
   const int frame_end = P.frame_begin + P.n_frames;
 
   bool need = true;  // lane wants a pixel
-  int x = 0, y = 0;
-  uint32_t lidx = 0, pix = 0;
-  int f = 0;
+  uint32_t lidx = 0;
   f3 acc = mk(0, 0, 0);
   uint32_t item_rays = 0;
-  // path state
+  Path path;
+  path.k0 = P.seed_lo;
+  path.k1 = P.seed_hi;
+  path.pix = 0;
+  path.start(0);
+  path.r0 = path.r1 = path.r2 = path.r3 = 0;
   f3 ro = mk(0, 0, 0), rd = mk(0, 0, 1), thr = mk(1, 1, 1);
   float rtime = 0.0f;
   int depth_left = 0;
-  Rng rng;
-  rng.init(0, 0, 0, 0);
   Counters cnt = {0, 0, 0, 0, 0, 0};
-  unsigned long long rays = 0, paths = 0;
+  uint32_t rays = 0, paths = 0;
   bool overflow = false;
 
+#if RT2_EXP_STAMPS
+  unsigned long long st_fetch = 0, st_trace = 0, st_shade = 0, st_finish = 0, st_t;
+#define RT2_STAMP(acc)                                   \
+  do {                                                   \
+    unsigned long long _n = __builtin_amdgcn_s_memtime(); \
+    acc += _n - st_t;                                    \
+    st_t = _n;                                           \
+  } while (0)
+#else
+#define RT2_STAMP(acc) \
+  do {                 \
+  } while (0)
+#endif
   while (true) {
+#if RT2_EXP_STAMPS
+    st_t = __builtin_amdgcn_s_memtime();
+#endif
     // ---- hand out pixels: one atomic per wave
     unsigned long long mask = __ballot(need);
     if (mask != 0ull) {
@@ -537,27 +794,25 @@ __global__ __launch_bounds__(kBlock) void render_kernel(const RenderParams P) {
         uint32_t item = base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
         if (item >= P.n_items) break;  // no work left for this lane
         uint32_t tile = item >> 6, within = item & 63u;
-        x = (int)((tile % (uint32_t)P.tiles_x) * 8u + (within & 7u));
+        int x = (int)((tile % (uint32_t)P.tiles_x) * 8u + (within & 7u));
         int r = (int)((tile / (uint32_t)P.tiles_x) * 8u + (within >> 3));
         if (x >= P.width || r >= P.local_rows) continue;  // partial edge tile
-        y = ((r / P.band_h) * P.world + P.rank) * P.band_h + (r % P.band_h);
+        int y = ((r / P.band_h) * P.world + P.rank) * P.band_h + (r % P.band_h);
         lidx = (uint32_t)r * (uint32_t)P.width + (uint32_t)x;
-        pix = (uint32_t)y * (uint32_t)P.width + (uint32_t)x;
+        path.pix = (uint32_t)y * (uint32_t)P.width + (uint32_t)x;
         acc = mk(P.accum[3 * lidx], P.accum[3 * lidx + 1], P.accum[3 * lidx + 2]);
         item_rays = 0;
-        f = P.frame_begin;
+        if (P.frame_begin >= frame_end) continue;  // zero frames requested
         need = false;
-        if (f >= frame_end) {
-          need = true;  // zero frames requested
-          continue;
-        }
-        rng.init(P.seed_lo, P.seed_hi, pix, (uint32_t)f);
-        camera_ray(P, x, y, f % sq, f / sq % sq, rng, ro, rd, rtime);
+        int f = P.frame_begin;
+        path.start((uint32_t)f);
+        camera_ray<F>(P, f % sq, f / sq % sq, path, ro, rd, rtime);
         thr = mk(1, 1, 1);
         depth_left = P.max_depth;
       }
     }
     if (need) continue;
+    RT2_STAMP(st_fetch);
 
     // ---- one bounce (RayColor, RayTracer.cpp:20-45)
     bool done = false;
@@ -566,27 +821,40 @@ __global__ __launch_bounds__(kBlock) void render_kernel(const RenderParams P) {
       done = true;  // RayColor(depth <= 0) returns 0 without casting a ray
     } else {
       item_rays++;
-      rays++;
-      Hit h;
-      if (!trace<kStats>(P, ro, rd, rtime, rng, h, stk, cnt, overflow)) {
+      HitRef h;
+      bool hit;
+      if constexpr (kMode == kModeLinear) {
+        hit = trace_linear<F, kStats>(P, ro, rd, rtime, path, h, cnt);
+      } else {
+        hit = trace_stack<F, kMode, kStats>(P, N, ro, rd, rtime, path, h, stk, cnt, overflow);
+      }
+      RT2_STAMP(st_trace);
+      if (!hit) {
         color = thr * bg;
         done = true;
       } else {
-        float4 m0 = M[2 * h.mat], m1 = M[2 * h.mat + 1];
+        f3 hp, hn;
+        bool front;
+        uint32_t mat;
+        resolve_hit<F>(N, h, ro, rd, rtime, hp, hn, front, mat);
+        float4 m0 = M[2 * mat], m1 = M[2 * mat + 1];
         uint32_t type = bits(m0.x);
         if (type == kMatDiffuseLight) {
-          color = thr * tex_value(P, bits(m1.z), h.p);
+          color = thr * tex_value<F>(P, bits(m1.z), hp);
           done = true;
         } else {
           f3 att, dir;
-          if (type == kMatMetal) {
-            dir = normalize(reflect(rd, h.n)) + (m1.x * rand_unit_vec3(rng));
+          bool dielectric = Has<F, kFeatSpecular>() && type == kMatDielectric;
+          f3 ru = mk(0.0f, 0.0f, 0.0f);
+          if (!dielectric) ru = rand_unit_vec3(path);  // one sampling site for every other material
+          if (Has<F, kFeatSpecular>() && type == kMatMetal) {
+            dir = normalize(reflect(rd, hn)) + (m1.x * ru);
             att = mk(m0.y, m0.z, m0.w);
-          } else if (type == kMatDielectric) {
+          } else if (dielectric) {
             att = mk(1.0f, 1.0f, 1.0f);
-            float ri = h.front ? m1.w : m1.y;
+            float ri = front ? m1.w : m1.y;
             f3 ud = normalize(rd);
-            float cos_t = gmin(dot(-ud, h.n), 1.0f);
+            float cos_t = gmin(dot(-ud, hn), 1.0f);
             float sin_t = sqrtf(1.0f - cos_t * cos_t);
             bool refl = ri * sin_t > 1.0f;
             if (!refl) {
@@ -596,31 +864,32 @@ __global__ __launch_bounds__(kBlock) void render_kernel(const RenderParams P) {
               double x2 = xx * xx;
               double x5 = (x2 * x2) * xx;
               double schlick = (double)r0 + (double)(1.0f - r0) * x5;
-              refl = schlick > (double)rng.uniform();
+              refl = schlick > (double)path.uniform();
             }
-            dir = refl ? reflect(ud, h.n) : refract(ud, h.n, ri);
-          } else if (type == kMatIsotropic) {
-            dir = rand_unit_vec3(rng);
-            att = tex_value(P, bits(m1.z), h.p);
+            dir = refl ? reflect(ud, hn) : refract(ud, hn, ri);
+          } else if (Has<F, kFeatMedium>() && type == kMatIsotropic) {
+            dir = ru;
+            att = tex_value<F>(P, bits(m1.z), hp);
           } else {  // Lambertian / Texture
-            dir = h.n + rand_unit_vec3(rng);
-            if (near_zero(dir)) dir = h.n;
-            att = (type == kMatLambertian) ? mk(m0.y, m0.z, m0.w) : tex_value(P, bits(m1.z), h.p);
+            dir = hn + ru;
+            if (near_zero(dir)) dir = hn;
+            att = (type == kMatLambertian) ? mk(m0.y, m0.z, m0.w) : tex_value<F>(P, bits(m1.z), hp);
           }
           thr = thr * att;
-          ro = h.p;
+          ro = hp;
           rd = dir;
           depth_left--;
         }
       }
     }
+    RT2_STAMP(st_shade);
     if (done) {
       acc = acc + color;
       paths++;
-      f++;
+      int f = (int)path.frame + 1;
       if (f < frame_end) {
-        rng.init(P.seed_lo, P.seed_hi, pix, (uint32_t)f);
-        camera_ray(P, x, y, f % sq, f / sq % sq, rng, ro, rd, rtime);
+        path.start((uint32_t)f);
+        camera_ray<F>(P, f % sq, f / sq % sq, path, ro, rd, rtime);
         thr = mk(1, 1, 1);
         depth_left = P.max_depth;
       } else {
@@ -629,8 +898,7 @@ __global__ __launch_bounds__(kBlock) void render_kernel(const RenderParams P) {
         P.accum[3 * lidx + 1] = acc.y;
         P.accum[3 * lidx + 2] = acc.z;
         if (P.pixels) {
-          float fi = (float)frame_end;
-          f3 c = acc / fi;
+          f3 c = acc / (float)frame_end;
           float cc[3] = {c.x, c.y, c.z};
           uint32_t rgba = 0xFF000000u;
 #pragma unroll
@@ -641,13 +909,23 @@ __global__ __launch_bounds__(kBlock) void render_kernel(const RenderParams P) {
           reinterpret_cast<uint32_t*>(P.pixels)[lidx] = rgba;
         }
         if (P.ray_counts) P.ray_counts[lidx] += item_rays;
+        rays += item_rays;
         need = true;
       }
     }
+    RT2_STAMP(st_finish);
   }
 
-  atomicAdd(P.stats + StatsCounters::kRays, rays);
-  atomicAdd(P.stats + StatsCounters::kPaths, paths);
+#if RT2_EXP_STAMPS
+  if (lane == __builtin_amdgcn_readfirstlane(lane)) {
+    atomicAdd(P.stats + 9, st_fetch);
+    atomicAdd(P.stats + 10, st_trace);
+    atomicAdd(P.stats + 11, st_shade);
+    atomicAdd(P.stats + 12, st_finish);
+  }
+#endif
+  atomicAdd(P.stats + StatsCounters::kRays, (unsigned long long)rays);
+  atomicAdd(P.stats + StatsCounters::kPaths, (unsigned long long)paths);
   if (kStats) {
     atomicAdd(P.stats + StatsCounters::kBvhTests, (unsigned long long)cnt.bvh);
     atomicAdd(P.stats + StatsCounters::kQuadTests, (unsigned long long)cnt.quad);
@@ -659,26 +937,81 @@ __global__ __launch_bounds__(kBlock) void render_kernel(const RenderParams P) {
   if (overflow) atomicAdd(P.stats + StatsCounters::kCount, 1ull);  // overflow flag slot
 }
 
+// ------------------------------------------------------------------------------------------
+// Instantiated feature sets (a launch picks the smallest superset of the scene's features).
+constexpr uint32_t kVariants[] = {
+    kFeatXform,                                   // Cornell box
+    kFeatXform | kFeatMedium,                     // Cornell volume
+    kFeatSphere | kFeatSpecular | kFeatDefocus,   // RTIOW book 1
+    kFeatAll,                                     // everything (book 2, scene graphs, textures)
+};
+constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
+
+using KernelFn = void (*)(RenderParams);
+
+template <int V, int kMode>
+KernelFn Pick(bool stats) {
+  return stats ? reinterpret_cast<KernelFn>(&render_kernel<kVariants[V], kMode, true>)
+               : reinterpret_cast<KernelFn>(&render_kernel<kVariants[V], kMode, false>);
+}
+
+template <int V>
+KernelFn PickMode(int mode, bool stats) {
+  switch (mode) {
+    case kModeStackLds: return Pick<V, kModeStackLds>(stats);
+    case kModeLinear: return Pick<V, kModeLinear>(stats);
+    default: return Pick<V, kModeStackGlobal>(stats);
+  }
+}
+
+KernelFn Kernel(int v, int mode, bool stats) {
+  switch (v) {
+    case 0: return PickMode<0>(mode, stats);
+    case 1: return PickMode<1>(mode, stats);
+    case 2: return PickMode<2>(mode, stats);
+    case 3: return PickMode<3>(mode, stats);
+  }
+  return nullptr;
+}
+
 }  // namespace dev
 
-// Launch entry used by capi.cpp. grid = resident workgroups (persistent lanes).
-hipError_t LaunchRender(const RenderParams& p, bool stats, int grid, hipStream_t stream) {
-  if (stats) {
-    hipLaunchKernelGGL(dev::render_kernel<true>, dim3(grid), dim3(dev::kBlock), 0, stream, p);
-  } else {
-    hipLaunchKernelGGL(dev::render_kernel<false>, dim3(grid), dim3(dev::kBlock), 0, stream, p);
+int RenderVariant(uint32_t features) {
+  int best = dev::kNumVariants - 1;
+  for (int v = 0; v < dev::kNumVariants; v++) {
+    if ((dev::kVariants[v] & features) == features &&
+        __builtin_popcount(dev::kVariants[v]) < __builtin_popcount(dev::kVariants[best]))
+      best = v;
   }
+  return best;
+}
+
+uint32_t RenderVariantFeatures(int v) { return dev::kVariants[v]; }
+
+int RenderMode(const RenderParams& p) {
+  if (p.lin_len) return kModeLinear;
+  return p.lds_nodes ? kModeStackLds : kModeStackGlobal;
+}
+
+size_t RenderLdsBytes(const RenderParams& p) {
+  if (p.lin_len) return 0;
+  return (size_t)p.lds_nodes * 16 + (size_t)p.stack_depth * dev::kBlock * 4;
+}
+
+// Launch entry used by capi.cpp. grid = resident workgroups (persistent lanes).
+hipError_t LaunchRender(const RenderParams& p, int variant, bool stats, int grid, hipStream_t stream) {
+  dev::KernelFn fn = dev::Kernel(variant, RenderMode(p), stats);
+  if (!fn) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(fn, dim3(grid), dim3(dev::kBlock), RenderLdsBytes(p), stream, p);
   return hipGetLastError();
 }
 
-int RenderBlocksPerCU(bool stats) {
+int RenderBlocksPerCU(int variant, int mode, bool stats, size_t lds_bytes) {
   int n = 0;
-  hipError_t e;
-  if (stats) {
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, dev::render_kernel<true>, dev::kBlock, 0);
-  } else {
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, dev::render_kernel<false>, dev::kBlock, 0);
-  }
+  dev::KernelFn fn = dev::Kernel(variant, mode, stats);
+  if (!fn) return 1;
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(fn), dev::kBlock,
+                                                             lds_bytes);
   return e == hipSuccess && n > 0 ? n : 1;
 }
 

@@ -57,7 +57,38 @@ enum MaterialType : uint32_t {
 // noise_type bits) (perlin vec offset bits, perlin perm offset bits, point_count bits, 0)
 enum TextureType : uint32_t { kTexSolid = 0, kTexChecker = 1, kTexNoise = 2 };
 
-constexpr int kTraversalStack = 24;  // entries per lane (LDS); compile.cpp proves the bound
+constexpr int kTraversalStack = 24;  // max entries per lane (LDS); compile.cpp proves the bound
+
+// Scene feature bits. The render kernel is instantiated for a few feature sets; a launch uses the
+// smallest instantiated superset of the scene's features, so code (and registers) for absent
+// features is not compiled into the kernel that runs.
+enum Feature : uint32_t {
+  kFeatSphere = 1u << 0,    // Sphere primitives (incl. motion)
+  kFeatMedium = 1u << 1,    // ConstantMedium + Isotropic
+  kFeatXform = 1u << 2,     // TransformedHittable
+  kFeatNoise = 1u << 3,     // Noise (Perlin / marble) textures
+  kFeatChecker = 1u << 4,   // Checker textures
+  kFeatSpecular = 1u << 5,  // Metal / Dielectric materials
+  kFeatDefocus = 1u << 6,   // thin-lens camera (defocus_angle > 0)
+  kFeatGenList = 1u << 7,   // lists whose children are not all quads/spheres (pushed on the stack)
+  kFeatAll = 0xFFu,
+};
+constexpr int kLdsSceneBytesMax = 96 * 1024;  // scenes up to this size are staged in LDS
+
+// Threaded ("linear") traversal program: the reference's fixed left-then-right pre-order of the
+// scene tree, one 16-byte entry per step: (kind, skip, record offset, aux).
+//   kind kBvh: skip = index after the node's subtree (taken when the AABB test misses)
+//   kind kQuad / kSphere / kMedium: record of the primitive; the next step is always index + 1;
+//     for kQuad, aux = length of the run of consecutive quads starting here with no skip target
+//     inside it (tested as a batch: the candidate math of two quads is interleaved)
+//   kind kXform: enter the transform (record = XFORM record); kXformExit: leave it
+//     (record = XFORM record, aux = parent XFORM ref or kRefNone)
+// Lists vanish (their children follow each other); span-1 leaves with a medium appear twice.
+// All lanes of a wave walk this array in lockstep at the smallest pending index, so the step
+// kind is wave-uniform and its record is read with scalar loads.
+constexpr int kLinearMaxSteps = 1024;  // scenes whose program is longer use the stack traversal
+
+enum TraversalMode : int { kModeStackGlobal = 0, kModeStackLds = 1, kModeLinear = 2 };
 
 struct CameraParams {
   float pixel00[3], du[3], dv[3], center[3], defocus_u[3], defocus_v[3];
@@ -91,6 +122,10 @@ struct RenderParams {
   uint32_t* ray_counts;    // optional: += rays per local pixel
   uint32_t* work_counter;  // zeroed before launch
   unsigned long long* stats;  // StatsCounters::kCount slots
+  int stack_depth;         // traversal-stack entries per lane (<= kTraversalStack)
+  uint32_t lds_nodes;      // float4 records staged in LDS (0: read the scene from global memory)
+  const void* lin;         // uint4[lin_len] threaded traversal program (kModeLinear)
+  uint32_t lin_len;
 };
 
 }  // namespace rt2

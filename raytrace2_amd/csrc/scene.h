@@ -142,6 +142,8 @@ struct CompiledScene {
   int max_stack = 0;              // proven traversal-stack bound (entries)
   int bvh_nodes = 0, quads = 0, spheres = 0, lists = 0, xforms = 0, media = 0;
   int bvh_depth = 0;
+  uint32_t features = 0;          // rt2_layout.h Feature bits (defocus is added per render)
+  std::vector<uint32_t> lin;      // threaded traversal program (4 words per step), empty if too long
 };
 bool CompileScene(const Scene& s, CompiledScene& out, std::string& err);
 
