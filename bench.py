@@ -86,30 +86,15 @@ def main():
     tr.synchronize()
     setup_s = time.perf_counter() - t0
     rows = tr.local_rows()
-    max_rows = -(-a.height // (a.band_h * world)) * a.band_h  # upper bound of rows per rank
-    local = torch.zeros((max_rows, a.width, 3), dtype=torch.float32, device=dev)
-    gathered = [torch.zeros_like(local) for _ in range(world)] if rank == 0 else None
-    image = torch.zeros((a.height, a.width, 3), dtype=torch.float32, device=dev) if rank == 0 else None
-    row_index = None
-    if rank == 0:
-        idx = []
-        for r in range(world):
-            ys = R.local_rows(a.height, a.band_h, r, world)
-            idx.append(torch.tensor(ys, dtype=torch.long, device=dev))
-        row_index = idx
+    from raytrace2_amd.dist import BandGather
+    gath = BandGather(a.height, a.width, a.band_h, world, rank, dev)
+    assert gath.local_view().shape[0] == rows
 
     def step():
         tr.Reset()
         tr.Render(a.spp)
-        tr.copy_accum_to(local.data_ptr(), stream.cuda_stream)
-        if world > 1:
-            dist.gather(local, gathered if rank == 0 else None, dst=0)
-            if rank == 0:
-                for r in range(world):
-                    n = row_index[r].numel()
-                    image.index_copy_(0, row_index[r], gathered[r][:n])
-        else:
-            image[:rows].copy_(local[:rows])
+        tr.copy_accum_to(gath.send.data_ptr(), stream.cuda_stream)
+        gath.gather()  # RCCL gather of the row bands to rank 0 + de-interleave
 
     for _ in range(a.warmup):
         step()
@@ -145,7 +130,7 @@ def main():
         rays_total = float(rays_local)
 
     if rank == 0 and a.out_image:
-        img = image.cpu().numpy() / np.float32(a.spp)
+        img = gath.image.cpu().numpy() / np.float32(a.spp)
         R.WriteImage(img, a.width, a.height, a.out_image)
 
     # ---- algorithmic bytes per ray from a stats pass (same seed, same kernel family) ----

@@ -236,16 +236,43 @@ void Json::set(const std::string& key, Json v) {
   obj_.emplace_back(key, std::move(v));
 }
 
+// Shortest round-trip decimal of v, laid out like nlohmann::json (grisu2 digits + format_buffer:
+// fixed notation for decimal exponents in (-4, 15], "x.0" for integral values, else d.ddde+XX).
 static std::string ShortestDouble(double v) {
   if (std::isnan(v) || std::isinf(v)) return "null";  // nlohmann writes null for non-finite
+  if (v == 0.0) return std::signbit(v) ? "-0.0" : "0.0";
   char buf[64];
-  for (int prec = 1; prec <= 17; prec++) {
-    snprintf(buf, sizeof(buf), "%.*g", prec, v);
+  int prec = 1;
+  for (; prec <= 17; prec++) {
+    snprintf(buf, sizeof(buf), "%.*e", prec - 1, v);
     if (strtod(buf, nullptr) == v) break;
   }
-  std::string s(buf);
-  if (s.find_first_of(".eEn") == std::string::npos) s += ".0";
-  return s;
+  std::string e(buf);
+  bool neg = e[0] == '-';
+  if (neg) e.erase(0, 1);
+  size_t epos = e.find('e');
+  int exp10 = atoi(e.c_str() + epos + 1);
+  std::string digits;
+  for (size_t k = 0; k < epos; k++)
+    if (e[k] != '.') digits.push_back(e[k]);
+  while (digits.size() > 1 && digits.back() == '0') digits.pop_back();
+  int len = (int)digits.size();
+  int n = exp10 + 1;  // position of the decimal point relative to the digits
+  std::string out;
+  if (len <= n && n <= 15) {
+    out = digits + std::string((size_t)(n - len), '0') + ".0";
+  } else if (0 < n && n <= 15) {
+    out = digits.substr(0, (size_t)n) + "." + digits.substr((size_t)n);
+  } else if (-4 < n && n <= 0) {
+    out = "0." + std::string((size_t)(-n), '0') + digits;
+  } else {
+    out = digits.substr(0, 1);
+    if (len > 1) out += "." + digits.substr(1);
+    char eb[16];
+    snprintf(eb, sizeof(eb), "e%c%02d", n - 1 < 0 ? '-' : '+', std::abs(n - 1));
+    out += eb;
+  }
+  return neg ? "-" + out : out;
 }
 
 void Json::DumpTo(std::string& out, int indent, int level) const {

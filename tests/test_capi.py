@@ -1,0 +1,63 @@
+"""The drop-in boundary: librt2.so loads, exports every function include/rt2.h declares, and
+reports errors through status codes + rt2_last_error (never aborts). No GPU compute here."""
+import ctypes
+import os
+import subprocess
+
+import pytest
+
+import raytrace2_amd as R
+from conftest import ROOT, scene_path
+
+
+def test_every_declared_symbol_is_exported():
+    names = R.declared_symbols()
+    assert len(names) >= 40
+    missing = [n for n in names if not hasattr(R.lib, n)]
+    assert not missing
+    # and nothing else with the rt2_ prefix is exported by accident (nm -D)
+    out = subprocess.run(["nm", "-D", "--defined-only", R._native.LIB_PATH], capture_output=True, text=True).stdout
+    exported = {l.split()[-1] for l in out.splitlines() if " T rt2_" in l}
+    assert exported == set(names)
+
+
+def test_header_is_plain_c():
+    # the header compiles as C99 with no HIP/torch includes
+    src = os.path.join(ROOT, "include", "rt2.h")
+    r = subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-fsyntax-only", "-x", "c", src],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    import re
+    txt = open(src).read()
+    assert set(re.findall(r"#include\s*<([^>]+)>", txt)) == {"stddef.h", "stdint.h"}
+    code = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    assert "hipStream_t" not in code and "torch" not in code.lower()
+
+
+def test_null_arguments_return_invalid():
+    assert R.lib.rt2_scene_load(None, 0, None) == -1
+    assert b"null" in R.lib.rt2_last_error()
+    assert R.lib.rt2_tracer_render(None, 1) == -1
+    assert R.lib.rt2_write_image(None, 1, 1, b"/tmp/x.png", 1) == -1
+
+
+def test_tracer_create_without_gpu_fails_cleanly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    s = R.Scene(scene_path("cornell_box_original"))
+    with pytest.raises(R.Rt2Error) as e:
+        R.RayTracer(s, 0)
+    assert e.value.code == -4  # RT2_ERR_HIP
+
+
+def test_version_string():
+    assert b"gfx950" in R.lib.rt2_version()
+
+
+def test_cpp_mirror_header_compiles():
+    # include/rt2/RayTracer.hpp: the C++ drop-in mirror of cpu::RayTracer over the C ABI
+    src = os.path.join(ROOT, "tests", "cpp", "mirror_compile.cpp")
+    r = subprocess.run(["g++", "-std=c++17", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+                        "-fsyntax-only", src], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr

@@ -1,0 +1,55 @@
+"""N>1 path on the CPU: world_size-2 gloo process group running the same band partition + gather
+(raytrace2_amd.dist.BandGather) the bench uses over RCCL. Each rank renders its row bands with the
+CPU restatement (stand-in renderer, no GPU here); the gathered image must equal the single-process
+render bit for bit, because sample streams are keyed by global pixel and frame."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import ROOT, scene_path
+
+W, H, BAND, SPP, FRAMES = 40, 45, 8, 16, 3
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out_path):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from raytrace2_amd.dist import BandGather
+    from oracle.oracle import OracleScene
+    g = BandGather(H, W, BAND, world, rank, torch.device("cpu"))
+    acc, _, _ = OracleScene(scene_path("cornell_box_original")).render(W, H, SPP, FRAMES, band_h=BAND, rank=rank,
+                                                                       world=world, forward=True)
+    assert acc.shape[0] == g.local_view().shape[0]
+    g.local_view().copy_(torch.from_numpy(acc))
+    img = g.gather()
+    if rank == 0:
+        np.save(out_path, img.numpy())
+    else:
+        assert img is None
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_band_gather_equals_single_render(tmp_path, world):
+    out = str(tmp_path / "img.npy")
+    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    img = np.load(out)
+    from oracle.oracle import OracleScene
+    full, _, _ = OracleScene(scene_path("cornell_box_original")).render(W, H, SPP, FRAMES, forward=True)
+    assert np.array_equal(img.view(np.uint32), full.view(np.uint32))
