@@ -65,6 +65,14 @@ def declared_symbols(header: str = HEADER_PATH):
 
 
 def _load():
+    # One HIP runtime per process: torch's libraries load torch/lib/libamdhip64.so by the name
+    # "libamdhip64.so"; librt2 asks for the SONAME libamdhip64.so.7, which the dynamic linker then
+    # resolves to that same already-loaded copy. Loading librt2 first would pull in
+    # /opt/rocm/lib's runtime and torch would add its own beside it.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"raytrace2_amd: {LIB_PATH} is missing — run `python -c 'import __graft_entry__ as g; "
                           f"g.build()'` (or make -C raytrace2_amd/csrc); there is no CPU fallback")

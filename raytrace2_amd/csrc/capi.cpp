@@ -41,6 +41,7 @@ struct rt2_tracer {
   void* d_perlin_vec = nullptr;
   int* d_perlin_perm = nullptr;
   void* d_lin = nullptr;
+  void* d_lind = nullptr;
   uint32_t lin_len = 0;
   bool use_linear = true;
   uint32_t root = kRefNone;
@@ -376,6 +377,7 @@ int rt2_tracer_create(const rt2_scene* s, int device, rt2_tracer** out) {
   if ((rc = Upload(&t->d_perlin_perm, c.perlin_perm.data(), c.perlin_perm.size() * sizeof(int))) != RT2_OK) return rc;
   if (!c.lin.empty()) {
     if ((rc = Upload(&t->d_lin, c.lin.data(), c.lin.size() * sizeof(uint32_t))) != RT2_OK) return rc;
+    if ((rc = Upload(&t->d_lind, c.lind.data(), c.lind.size() * sizeof(float))) != RT2_OK) return rc;
     t->lin_len = (uint32_t)(c.lin.size() / 4);
   }
   HIP_TRY(hipMalloc(&t->d_work, 64));
@@ -419,6 +421,7 @@ void rt2_tracer_destroy(rt2_tracer* t) {
   (void)hipFree(t->d_perlin_vec);
   (void)hipFree(t->d_perlin_perm);
   (void)hipFree(t->d_lin);
+  (void)hipFree(t->d_lind);
   (void)hipFree(t->d_work);
   (void)hipFree(t->d_stats);
   if (t->own_stream) (void)hipStreamDestroy(t->own_stream);
@@ -525,6 +528,7 @@ int rt2_tracer_render(rt2_tracer* t, int n_frames) {
   bool lds = t->use_lds && (size_t)t->node_records * 16 <= (size_t)kLdsSceneBytesMax;
   p.lds_nodes = lds ? t->node_records : 0u;
   p.lin = t->d_lin;
+  p.lind = t->d_lind;
   p.lin_len = t->use_linear ? t->lin_len : 0u;
   uint32_t feats = t->features | (p.cam.defocus_angle > 0.0f ? (uint32_t)kFeatDefocus : 0u);
   int variant = RenderVariant(feats);

@@ -178,38 +178,71 @@ struct Flattener {
     return ref;
   }
 
-  // Threaded program (rt2_layout.h): pre-order of the tree the reference traverses. Returns
-  // false when the program would exceed kLinearMaxSteps.
-  bool Linearize(int i, uint32_t parent_xf, std::vector<uint32_t>& lin) {
+  // Threaded program (rt2_layout.h): pre-order of the tree the reference traverses, plus a copy of
+  // every visited record in program order (`lind`), so consecutive steps read consecutive bytes.
+  // References inside copied records (XFORM parent, medium boundary) point into `lind`.
+  // Returns false when the program would exceed kLinearMaxSteps.
+  uint32_t CopyRecords(uint32_t src_off, int n, std::vector<float>& lind) {
+    uint32_t off = (uint32_t)(lind.size() / 4);
+    const float* r = out.nodes.data() + 4 * (size_t)src_off;
+    lind.insert(lind.end(), r, r + 4 * n);
+    return off;
+  }
+  // copies a medium boundary (quad, sphere, or a leaf-only list) and returns its lind ref
+  uint32_t CopyBoundary(int i, std::vector<float>& lind) {
+    const Obj& o = s.objs[(size_t)i];
+    uint32_t src = ref_of.at(i) & kOffsetMask;
+    if (o.kind == kQuad) return make_ref(kQuad, CopyRecords(src, kQuadRecords, lind));
+    if (o.kind == kSphere) return make_ref(kSphere, CopyRecords(src, kSphereRecords, lind));
+    std::vector<uint32_t> kids;
+    for (int c : o.children) kids.push_back(CopyBoundary(c, lind));
+    uint32_t off = CopyRecords(src, 1 + (int)((kids.size() + 3) / 4), lind);
+    for (size_t k = 0; k < kids.size(); k++) lind[4 * (off + 1 + k / 4) + k % 4] = Bits(kids[k]);
+    return make_ref(kList, off);
+  }
+  bool Linearize(int i, uint32_t parent_xf, std::vector<uint32_t>& lin, std::vector<float>& lind) {
     if (lin.size() / 4 >= (size_t)kLinearMaxSteps) return false;
     const Obj& o = s.objs[(size_t)i];
-    uint32_t ref = ref_of.at(i);
-    uint32_t off = ref & kOffsetMask;
+    uint32_t src = ref_of.at(i) & kOffsetMask;
     auto emit = [&](uint32_t kind, uint32_t rec, uint32_t aux) {
       lin.insert(lin.end(), {kind, 0u, rec, aux});
       return lin.size() / 4 - 1;
     };
     switch (o.kind) {
       case kBvh: {
-        size_t me = emit(kBvh, off, 0);
-        if (!Linearize(o.left, parent_xf, lin)) return false;
+        size_t me = emit(kBvh, CopyRecords(src, kBvhRecords, lind), 0);
+        if (!Linearize(o.left, parent_xf, lin, lind)) return false;
         if (!(o.left == o.right && !HasMedium(o.left))) {
-          if (!Linearize(o.right, parent_xf, lin)) return false;
+          if (!Linearize(o.right, parent_xf, lin, lind)) return false;
         }
         lin[4 * me + 1] = (uint32_t)(lin.size() / 4);
         return true;
       }
       case kList:
         for (int c : o.children)
-          if (!Linearize(c, parent_xf, lin)) return false;
+          if (!Linearize(c, parent_xf, lin, lind)) return false;
         return true;
-      case kXform:
+      case kXform: {
+        uint32_t off = CopyRecords(src, kXformRecords, lind);
+        lind[4 * (off + 1) + 3] = Bits(parent_xf);
+        uint32_t self = make_ref(kXform, off);
         emit(kXform, off, 0);
-        if (!Linearize(o.child, ref, lin)) return false;
+        if (!Linearize(o.child, self, lin, lind)) return false;
         emit(kXformExit, off, parent_xf);
         return true;
-      default:  // quad, sphere, medium (boundary evaluated inline)
-        emit(o.kind, off, 0);
+      }
+      case kMedium: {
+        uint32_t off = CopyRecords(src, kMediumRecords, lind);
+        uint32_t b = CopyBoundary(o.child, lind);
+        lind[4 * off + 2] = Bits(b);
+        emit(kMedium, off, 0);
+        return lin.size() / 4 <= (size_t)kLinearMaxSteps;
+      }
+      case kQuad:
+        emit(kQuad, CopyRecords(src, kQuadRecords, lind), 0);
+        return lin.size() / 4 <= (size_t)kLinearMaxSteps;
+      default:  // sphere
+        emit(kSphere, CopyRecords(src, kSphereRecords, lind), 0);
         return lin.size() / 4 <= (size_t)kLinearMaxSteps;
     }
   }
@@ -317,7 +350,10 @@ bool CompileScene(const Scene& s, CompiledScene& out, std::string& err) {
     err = "scene too large for 28-bit node offsets";
     return false;
   }
-  if (!fl.Linearize(s.root, kRefNone, out.lin)) out.lin.clear();
+  if (!fl.Linearize(s.root, kRefNone, out.lin, out.lind)) {
+    out.lin.clear();
+    out.lind.clear();
+  }
   // Quad runs: for a quad step, aux = number of consecutive quad steps starting there with no
   // skip target inside the run (so every lane that reaches the run's first step walks all of it).
   {

@@ -110,6 +110,45 @@ struct Nodes {
   }
 };
 
+// Scalar (SMEM) loads of wave-uniform data: the linear traversal's program entries and records
+// land in SGPRs. Inline asm because the compiler will not prove these loads unclobbered (the
+// kernel stores the accumulation buffer inside the same loop). Base and byte offset must be
+// wave-uniform; each helper waits for its own loads. Helpers issuing several loads mark their
+// outputs early-clobber: a later load's base/offset must not share registers with an earlier
+// load's destination (its data can land before the later load reads its operands).
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
+__device__ __forceinline__ u32x4 sld4(const void* base, uint32_t off) {
+  u32x4 v;
+  asm("s_load_dwordx4 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(base), "s"(off));
+  return v;
+}
+__device__ __forceinline__ u32x8 sld8(const void* base, uint32_t off) {
+  u32x8 v;
+  asm("s_load_dwordx8 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(base), "s"(off));
+  return v;
+}
+__device__ __forceinline__ u32x16 sld16(const void* base, uint32_t off) {
+  u32x16 v;
+  asm("s_load_dwordx16 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(base), "s"(off));
+  return v;
+}
+// 20 dwords (one quad record) at off
+__device__ __forceinline__ void sld20(const void* base, uint32_t off, u32x16& a, u32x4& b) {
+  asm("s_load_dwordx16 %0, %2, %3\n\ts_load_dwordx4 %1, %2, %4\n\ts_waitcnt lgkmcnt(0)"
+      : "=&s"(a), "=&s"(b)
+      : "s"(base), "s"(off), "s"(off + 64u));
+}
+// 40 dwords (two consecutive quad records) at off
+__device__ __forceinline__ void sld40(const void* base, uint32_t off, u32x16& a, u32x16& b, u32x8& c) {
+  asm("s_load_dwordx16 %0, %3, %4\n\ts_load_dwordx16 %1, %3, %5\n\ts_load_dwordx8 %2, %3, %6\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&s"(a), "=&s"(b), "=&s"(c)
+      : "s"(base), "s"(off), "s"(off + 64u), "s"(off + 128u));
+}
+__device__ __forceinline__ float uf(uint32_t u) { return __uint_as_float(u); }
+
 // ------------------------------------------------------------------------------------------
 // Philox4x32-10 path stream keyed by (seed, pixel, frame). Draws are taken in groups of K <= 4
 // consecutive values; `n` counts draws and the buffer holds the block of the last value drawn
@@ -289,6 +328,20 @@ __device__ __forceinline__ bool quad_cand(const Nodes<kMode>& N, uint32_t off, f
   f3 pv = p - xyz(r1);
   float alpha = dot(xyz(r4), cross(pv, xyz(r3)));
   float beta = dot(xyz(r4), cross(xyz(r2), pv));
+  t_out = t;
+  return !(fabsf(n_dot) <= 1e-8f) && (0.0f <= alpha && alpha <= 1.0f) && (0.0f <= beta && beta <= 1.0f);
+}
+
+// quad_cand on a record held in registers: w[0..19] = (n, D) (q, mat) (u, -) (v, -) (w, -)
+__device__ __forceinline__ bool quad_cand_w(const float* w, f3 o, f3 d, float& t_out) {
+  f3 n = mk(w[0], w[1], w[2]);
+  float n_dot = dot(n, d);
+  float t = (w[3] - dot(n, o)) / n_dot;
+  f3 p = o + d * t;
+  f3 pv = p - mk(w[4], w[5], w[6]);
+  f3 ww = mk(w[16], w[17], w[18]);
+  float alpha = dot(ww, cross(pv, mk(w[12], w[13], w[14])));
+  float beta = dot(ww, cross(mk(w[8], w[9], w[10]), pv));
   t_out = t;
   return !(fabsf(n_dot) <= 1e-8f) && (0.0f <= alpha && alpha <= 1.0f) && (0.0f <= beta && beta <= 1.0f);
 }
@@ -492,14 +545,15 @@ __device__ __forceinline__ bool trace_stack(const RenderParams& P, const Nodes<k
 
 // Threaded traversal (small scenes): all lanes of the wave walk the pre-order program P.lin in
 // lockstep. Each lane keeps the index of its next step; the wave executes the smallest pending
-// index, so the step kind is wave-uniform (no divergence between kinds) and the step's records are
-// scalar loads. A lane whose AABB test misses jumps to the node's skip index. Per lane the visit
-// order is exactly the stack traversal's.
+// index, so the step kind is wave-uniform (no divergence between kinds) and the step's program
+// entry and record are scalar loads into SGPRs. A lane whose AABB test misses jumps to the node's
+// skip index. Per lane the visit order is exactly the stack traversal's.
 template <uint32_t F, bool kStats>
 __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd, float time, Path& path, HitRef& h,
                                              Counters& cnt) {
-  const Nodes<kModeLinear> N{reinterpret_cast<const float4*>(P.nodes)};
-  const uint4* __restrict__ prog = reinterpret_cast<const uint4*>(P.lin);
+  const Nodes<kModeLinear> N{reinterpret_cast<const float4*>(P.lind)};  // boundaries / nested xforms
+  const void* prog = P.lin;
+  const void* recs = P.lind;
   f3 o = wo, d = wd;
   const f3 winv = mk(1.0f / wd.x, 1.0f / wd.y, 1.0f / wd.z);
   f3 inv = winv;
@@ -515,34 +569,60 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
     unsigned long long lower;
     while ((lower = __ballot(next < i)) != 0ull) i = __builtin_amdgcn_readlane(next, __ffsll((long long)lower) - 1);
     if (i >= len) break;
-    const uint4 st = prog[i];
+    const u32x4 st = sld4(prog, i * 16u);
     const uint32_t kind = st.x, off = st.z;
     if (next != i) continue;
     next = i + 1u;
     if (kind == kBvh) {
       if (kStats) cnt.bvh++;
-      if (!aabb_hit(N[off], N[off + 1], o, inv, tmin, tmax)) next = st.y;
+      const u32x8 b = sld8(recs, off * 16u);
+      float4 lo = make_float4(uf(b[0]), uf(b[1]), uf(b[2]), 0.0f), hi = make_float4(uf(b[4]), uf(b[5]), uf(b[6]), 0.0f);
+      if (!aabb_hit(lo, hi, o, inv, tmin, tmax)) next = st.y;
     } else if (kind == kQuad) {
-      // a run of st.w quads: two candidate computations in flight, applied in program order
+      // a run of st.w quads with contiguous records: two candidates in flight, applied in order
       const uint32_t run = st.w;
       for (uint32_t k = 0; k < run; k += 2) {
-        const uint32_t off0 = prog[i + k].z;
-        const bool two = k + 1 < run;
-        const uint32_t off1 = two ? prog[i + k + 1].z : off0;
+        const uint32_t o0 = off + 5u * k;
+        float w0[20], w1[20];
         float t0, t1;
-        bool ok0 = quad_cand(N, off0, o, d, t0);
-        bool ok1 = quad_cand(N, off1, o, d, t1) && two;
-        if (kStats) cnt.quad += two ? 2 : 1;
+        bool ok0, ok1 = false;
+        if (k + 1 < run) {
+          u32x16 a, b2;
+          u32x8 c;
+          sld40(recs, o0 * 16u, a, b2, c);
+#pragma unroll
+          for (int j = 0; j < 16; j++) w0[j] = uf(a[j]);
+#pragma unroll
+          for (int j = 0; j < 4; j++) w0[16 + j] = uf(b2[j]);
+#pragma unroll
+          for (int j = 0; j < 12; j++) w1[j] = uf(b2[4 + j]);
+#pragma unroll
+          for (int j = 0; j < 8; j++) w1[12 + j] = uf(c[j]);
+          ok0 = quad_cand_w(w0, o, d, t0);
+          ok1 = quad_cand_w(w1, o, d, t1);
+          if (kStats) cnt.quad += 2;
+        } else {
+          u32x16 a;
+          u32x4 b2;
+          sld20(recs, o0 * 16u, a, b2);
+#pragma unroll
+          for (int j = 0; j < 16; j++) w0[j] = uf(a[j]);
+#pragma unroll
+          for (int j = 0; j < 4; j++) w0[16 + j] = uf(b2[j]);
+          ok0 = quad_cand_w(w0, o, d, t0);
+          t1 = 0.0f;
+          if (kStats) cnt.quad += 1;
+        }
         if (ok0 && tmin <= t0 && t0 <= tmax) {
           tmax = t0;
           any = true;
-          h.prim = make_ref(kQuad, off0);
+          h.prim = make_ref(kQuad, o0);
           h.xf = cur_xf;
         }
         if (ok1 && tmin <= t1 && t1 <= tmax) {
           tmax = t1;
           any = true;
-          h.prim = make_ref(kQuad, off1);
+          h.prim = make_ref(kQuad, o0 + 5u);
           h.xf = cur_xf;
         }
       }
@@ -558,7 +638,14 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
       }
     } else if (Has<F, kFeatXform>() && kind == kXform) {
       if (kStats) cnt.xform++;
-      to_model(N, off, o, d);
+      const u32x16 m = sld16(recs, off * 16u);  // inverse-model columns
+      f3 no = mk((uf(m[0]) * o.x + uf(m[4]) * o.y) + (uf(m[8]) * o.z + uf(m[12])),
+                 (uf(m[1]) * o.x + uf(m[5]) * o.y) + (uf(m[9]) * o.z + uf(m[13])),
+                 (uf(m[2]) * o.x + uf(m[6]) * o.y) + (uf(m[10]) * o.z + uf(m[14])));
+      f3 nd = mk(uf(m[0]) * d.x + uf(m[4]) * d.y + uf(m[8]) * d.z, uf(m[1]) * d.x + uf(m[5]) * d.y + uf(m[9]) * d.z,
+                 uf(m[2]) * d.x + uf(m[6]) * d.y + uf(m[10]) * d.z);
+      o = no;
+      d = normalize(nd);
       inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
       cur_xf = make_ref(kXform, off);
     } else if (Has<F, kFeatXform>() && kind == kXformExit) {
@@ -836,7 +923,12 @@ __global__ __launch_bounds__(kBlock, RT2_MIN_WAVES_PER_EU) void render_kernel(co
         f3 hp, hn;
         bool front;
         uint32_t mat;
-        resolve_hit<F>(N, h, ro, rd, rtime, hp, hn, front, mat);
+        if constexpr (kMode == kModeLinear) {
+          resolve_hit<F>(Nodes<kModeLinear>{reinterpret_cast<const float4*>(P.lind)}, h, ro, rd, rtime, hp, hn, front,
+                         mat);
+        } else {
+          resolve_hit<F>(N, h, ro, rd, rtime, hp, hn, front, mat);
+        }
         float4 m0 = M[2 * mat], m1 = M[2 * mat + 1];
         uint32_t type = bits(m0.x);
         if (type == kMatDiffuseLight) {

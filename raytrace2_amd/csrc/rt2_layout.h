@@ -84,6 +84,8 @@ constexpr int kLdsSceneBytesMax = 96 * 1024;  // scenes up to this size are stag
 //   kind kXform: enter the transform (record = XFORM record); kXformExit: leave it
 //     (record = XFORM record, aux = parent XFORM ref or kRefNone)
 // Lists vanish (their children follow each other); span-1 leaves with a medium appear twice.
+// Record offsets refer to a separate record stream (RenderParams::lind) holding each step's
+// record in program order, so a run of quads is contiguous.
 // All lanes of a wave walk this array in lockstep at the smallest pending index, so the step
 // kind is wave-uniform and its record is read with scalar loads.
 constexpr int kLinearMaxSteps = 1024;  // scenes whose program is longer use the stack traversal
@@ -125,6 +127,7 @@ struct RenderParams {
   int stack_depth;         // traversal-stack entries per lane (<= kTraversalStack)
   uint32_t lds_nodes;      // float4 records staged in LDS (0: read the scene from global memory)
   const void* lin;         // uint4[lin_len] threaded traversal program (kModeLinear)
+  const void* lind;        // float4 records of the program's steps (kModeLinear)
   uint32_t lin_len;
 };
 

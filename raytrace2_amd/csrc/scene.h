@@ -144,6 +144,7 @@ struct CompiledScene {
   int bvh_depth = 0;
   uint32_t features = 0;          // rt2_layout.h Feature bits (defocus is added per render)
   std::vector<uint32_t> lin;      // threaded traversal program (4 words per step), empty if too long
+  std::vector<float> lind;        // records of the program's steps, in program order (float4)
 };
 bool CompileScene(const Scene& s, CompiledScene& out, std::string& err);
 

@@ -100,3 +100,21 @@ def test_full_size_rows_subset(have_gpu):
     o_acc, o_rc, _ = oracle_render("cornell_box_original", w, h, 1000, frames, band_h=16, rank=5, world=32)
     np.testing.assert_array_equal(rc, o_rc)
     assert np.array_equal(acc.view(np.uint32), o_acc.view(np.uint32))
+
+
+MODES = {"linear": {}, "stack_lds": {"RT2_NO_LINEAR": "1"}, "stack_global": {"RT2_NO_LINEAR": "1", "RT2_NO_LDS": "1"}}
+
+
+@pytest.mark.parametrize("mode", list(MODES))
+@pytest.mark.parametrize("name,w,h,spp,frames", [c for c in CASES if c[0] != "book2_final_scene_10000_samples"],
+                         ids=[c[0] for c in CASES if c[0] != "book2_final_scene_10000_samples"])
+def test_every_traversal_mode_matches(have_gpu, monkeypatch, mode, name, w, h, spp, frames):
+    """The threaded lockstep traversal and the stack traversal (LDS or global scene) visit nodes in
+    the same per-lane order, so every mode is bit-identical to the oracle."""
+    for k, v in MODES[mode].items():
+        monkeypatch.setenv(k, v)
+    acc, rc, st, _ = gpu_render(name, w, h, spp, min(frames, 4))
+    o_acc, o_rc, _ = oracle_render(name, w, h, spp, min(frames, 4), forward=True)
+    assert st["overflow"] == 0
+    np.testing.assert_array_equal(rc, o_rc)
+    assert np.array_equal(acc.view(np.uint32), o_acc.view(np.uint32))
