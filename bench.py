@@ -14,6 +14,7 @@ render kernel (algorithmic bytes per launch / HIP-event launch time vs 8 TB/s HB
 `cpu_baseline` object (the oracle restatement timed on this host's cores on a bounded sample).
 """
 import argparse
+import glob
 import json
 import os
 import sys
@@ -133,6 +134,7 @@ def main():
         img = gath.image.cpu().numpy() / np.float32(a.spp)
         R.WriteImage(img, a.width, a.height, a.out_image)
 
+    workload = f"{a.scene} {a.width}x{a.height} @ {a.spp} spp, max_depth {a.max_depth}"
     # ---- algorithmic bytes per ray from a stats pass (same seed, same kernel family) ----
     roofline = None
     if rank == 0:
@@ -151,18 +153,42 @@ def main():
         bytes_per_launch = rays_per_launch * b_ray + frame_bytes
         avg_launch_s = kernel_ms / 1e3 / launches
         achieved = bytes_per_launch / avg_launch_s / 1e9
+        traffic, traffic_src, valu_issue = None, None, None
+        for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json")), reverse=True):
+            try:
+                prof = json.load(open(f))
+                under = prof.get("bench_under_rocprof") or {}
+                if under.get("config", {}).get("workload") != workload or "hbm_bytes_per_launch" not in prof:
+                    continue
+                traffic = int(prof["hbm_bytes_per_launch"]["corrected"])
+                traffic_src = os.path.relpath(f, ROOT)
+                pmc = prof.get("pmc", {})
+                if "SQ_INSTS_VALU" in pmc and "GRBM_GUI_ACTIVE" in pmc:
+                    ms = pmc["dispatch_ms"]["pmc_SQ_WAVES_SQ_INSTS_VALU_SQ_INSTS_SALU_SQ_"]
+                    clock = pmc["GRBM_GUI_ACTIVE"] / 8 / (ms / 1e3)  # MI355X_MICROARCH.md: sum over 8 XCDs
+                    simds = 4 * 256
+                    valu_issue = pmc["SQ_INSTS_VALU"] * 2 / (simds * clock * ms / 1e3)  # wave64 = 2 cycles/SIMD32
+                break
+            except (OSError, ValueError, KeyError):
+                continue
         roofline = {
             "bound": "hbm",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, gfx950-corrected)",
+            "traffic_source": traffic_src,
+            "note": "algorithmic bytes = scene records touched per ray (SURVEY 8d) served from the scalar cache/L1; "
+                    "frac > 1 means that record traffic exceeds what HBM alone could feed; measured HBM traffic is "
+                    "`traffic`; the kernel is VALU-issue/latency bound (valu_issue_frac)",
+            "valu_issue_frac": None if valu_issue is None else round(valu_issue, 3),
             "kernel": "rt2::dev::render_kernel<false>",
             "avg_launch_ms": round(kernel_ms / launches, 3),
             "bytes_per_ray": round(b_ray, 1),
             "records_per_ray": {k: round(v, 3) for k, v in per_ray.items()},
-            "valu_frac": round(rays_per_launch * f_ray / avg_launch_s / 1e12 / FP32_VALU_PEAK_TFLOPS, 4),
+            "useful_flop_frac": round(rays_per_launch * f_ray / avg_launch_s / 1e12 / FP32_VALU_PEAK_TFLOPS, 4),
         }
 
     cpu = None
@@ -198,7 +224,7 @@ def main():
             "dtype": "f32",
             "data": "synthetic: committed scene JSON (scenes/), Philox4x32-10 sample streams seeded "
                     f"{a.seed:#x}",
-            "config": {"workload": f"{a.scene} {a.width}x{a.height} @ {a.spp} spp, max_depth {a.max_depth}",
+            "config": {"workload": workload,
                        "parallelism": f"row-bands h={a.band_h} x {world} GPU(s), RCCL gather to rank 0",
                        "launch_frames": a.launch_frames or a.spp},
             "roofline": roofline,
