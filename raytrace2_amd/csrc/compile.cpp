@@ -71,7 +71,14 @@ struct Flattener {
         uint32_t off = Alloc(kQuadRecords);
         Put(off, o.n.x, o.n.y, o.n.z, o.d);
         Put(off + 1, o.q.x, o.q.y, o.q.z, Bits(o.material));
-        Put(off + 2, o.u.x, o.u.y, o.u.z, 0);
+        // axis code k+1 when n and w have exact zeros off axis k (the kernel's exact axis-aligned test)
+        uint32_t axis = 0;
+        for (int k = 0; k < 3 && !axis; k++) {
+          int a = (k + 1) % 3, b = (k + 2) % 3;
+          if (o.n[a] == 0.0f && o.n[b] == 0.0f && o.w[a] == 0.0f && o.w[b] == 0.0f && o.n[k] != 0.0f)
+            axis = (uint32_t)k + 1;
+        }
+        Put(off + 2, o.u.x, o.u.y, o.u.z, Bits(axis));
         Put(off + 3, o.v.x, o.v.y, o.v.z, 0);
         Put(off + 4, o.w.x, o.w.y, o.w.z, 0);
         ref = make_ref(kQuad, off);

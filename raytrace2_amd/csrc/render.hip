@@ -346,6 +346,37 @@ __device__ __forceinline__ bool quad_cand_w(const float* w, f3 o, f3 d, float& t
   return !(fabsf(n_dot) <= 1e-8f) && (0.0f <= alpha && alpha <= 1.0f) && (0.0f <= beta && beta <= 1.0f);
 }
 
+// Axis-aligned Quad::Hit (record axis code K + 1): with n and w exactly zero off axis K,
+// dot(n, d), dot(n, o) and dot(w, cross(., .)) equal the single axis-K products in value (the
+// other terms are signed zeros, which no comparison distinguishes), so this returns the same
+// decision and t as quad_cand_w at a third of the arithmetic.
+template <int K>
+__device__ __forceinline__ float comp(f3 v) {
+  return K == 0 ? v.x : (K == 1 ? v.y : v.z);
+}
+template <int K>
+__device__ __forceinline__ bool quad_cand_aa(const float* w, f3 o, f3 d, float& t_out) {
+  constexpr int A = (K + 1) % 3, B = (K + 2) % 3;
+  const float nk = w[K], wk = w[16 + K];
+  float n_dot = nk * comp<K>(d);
+  float t = (w[3] - nk * comp<K>(o)) / n_dot;
+  float pva = (comp<A>(o) + comp<A>(d) * t) - w[4 + A];
+  float pvb = (comp<B>(o) + comp<B>(d) * t) - w[4 + B];
+  float alpha = wk * (pva * w[12 + B] - w[12 + A] * pvb);  // w . cross(pv, v)
+  float beta = wk * (w[8 + A] * pvb - pva * w[8 + B]);    // w . cross(u, pv)
+  t_out = t;
+  return !(fabsf(n_dot) <= 1e-8f) && (0.0f <= alpha && alpha <= 1.0f) && (0.0f <= beta && beta <= 1.0f);
+}
+// quad candidate dispatched on a wave-uniform axis code
+__device__ __forceinline__ bool quad_cand_u(uint32_t axis, const float* w, f3 o, f3 d, float& t) {
+  switch (axis) {
+    case 1: return quad_cand_aa<0>(w, o, d, t);
+    case 2: return quad_cand_aa<1>(w, o, d, t);
+    case 3: return quad_cand_aa<2>(w, o, d, t);
+    default: return quad_cand_w(w, o, d, t);
+  }
+}
+
 template <uint32_t F, int kMode>
 __device__ __forceinline__ bool prim_t(const Nodes<kMode>& N, uint32_t ref, f3 o, f3 d, float time, float tmin,
                                        float tmax, float& t, Counters& cnt) {
@@ -598,8 +629,8 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
           for (int j = 0; j < 12; j++) w1[j] = uf(b2[4 + j]);
 #pragma unroll
           for (int j = 0; j < 8; j++) w1[12 + j] = uf(c[j]);
-          ok0 = quad_cand_w(w0, o, d, t0);
-          ok1 = quad_cand_w(w1, o, d, t1);
+          ok0 = quad_cand_u(a[11], w0, o, d, t0);
+          ok1 = quad_cand_u(b2[15], w1, o, d, t1);
           if (kStats) cnt.quad += 2;
         } else {
           u32x16 a;
@@ -609,7 +640,7 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
           for (int j = 0; j < 16; j++) w0[j] = uf(a[j]);
 #pragma unroll
           for (int j = 0; j < 4; j++) w0[16 + j] = uf(b2[j]);
-          ok0 = quad_cand_w(w0, o, d, t0);
+          ok0 = quad_cand_u(a[11], w0, o, d, t0);
           t1 = 0.0f;
           if (kStats) cnt.quad += 1;
         }

@@ -33,7 +33,8 @@ inline constexpr uint32_t make_ref(uint32_t kind, uint32_t off) { return (kind <
 // Record layouts (each line one float4; "(bits)" = uint32 stored with __float_as_uint):
 //  BVH   : (min.xyz, left_ref bits) (max.xyz, right_ref bits)  right_ref = kRefNone when a
 //          span-1 leaf's duplicate test is provably a no-op (no medium below it).
-//  QUAD  : (n.xyz, D) (q.xyz, material bits) (u.xyz, 0) (v.xyz, 0) (w.xyz, 0)
+//  QUAD  : (n.xyz, D) (q.xyz, material bits) (u.xyz, axis bits) (v.xyz, 0) (w.xyz, 0)
+//          axis = k + 1 when n and w are exactly zero off axis k (exact axis-aligned test), else 0
 //  SPHERE: (c0.xyz, radius) (displacement.xyz, material bits)
 //  LIST  : (count bits, flags bits, 0, 0) then child refs, 4 per record. flags bit0 = every
 //          child is a QUAD or SPHERE (iterated inline, no stack traffic).
