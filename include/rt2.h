@@ -128,6 +128,7 @@ typedef struct {
   uint64_t launches;
   double kernel_ms;   /* sum of per-launch HIP event durations */
   uint64_t stamps[4]; /* diagnostic builds only: s_memtime sums (fetch, trace, shade, finish) */
+  uint64_t diag[8];   /* diagnostic builds only: per-wave traversal step counts */
 } rt2_stats;
 RT2_API int rt2_tracer_get_stats(rt2_tracer* tr, rt2_stats* out);
 RT2_API int rt2_tracer_reset_stats(rt2_tracer* tr);

@@ -49,12 +49,14 @@ class Stats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in
                 ("rays", "paths", "bvh_tests", "quad_tests", "sphere_tests", "xform_visits",
                  "medium_tests", "list_visits", "overflow", "launches")] + [("kernel_ms", ctypes.c_double),
-                                                                           ("stamps", ctypes.c_uint64 * 4)]
+                                                                           ("stamps", ctypes.c_uint64 * 4),
+                                                                           ("diag", ctypes.c_uint64 * 8)]
 
     def as_dict(self):
         d = {n: (getattr(self, n) if n == "kernel_ms" else int(getattr(self, n))) for n, _ in self._fields_
-             if n != "stamps"}
+             if n not in ("stamps", "diag")}
         d["stamps"] = [int(x) for x in self.stamps]
+        d["diag"] = [int(x) for x in self.diag]
         return d
 
 

@@ -381,8 +381,8 @@ int rt2_tracer_create(const rt2_scene* s, int device, rt2_tracer** out) {
     t->lin_len = (uint32_t)(c.lin.size() / 4);
   }
   HIP_TRY(hipMalloc(&t->d_work, 64));
-  HIP_TRY(hipMalloc(&t->d_stats, 16 * sizeof(unsigned long long)));
-  HIP_TRY(hipMemset(t->d_stats, 0, 16 * sizeof(unsigned long long)));
+  HIP_TRY(hipMalloc(&t->d_stats, kStatsSlots * sizeof(unsigned long long)));
+  HIP_TRY(hipMemset(t->d_stats, 0, kStatsSlots * sizeof(unsigned long long)));
   t->root = c.root;
   t->node_records = (uint32_t)(c.nodes.size() / 4);
   t->features = c.features;
@@ -644,7 +644,7 @@ int rt2_tracer_get_stats(rt2_tracer* t, rt2_stats* o) {
   if (!t || !o) return Fail(RT2_ERR_INVALID, "null argument");
   int rc = Sync(t);
   if (rc != RT2_OK) return rc;
-  unsigned long long s[16];
+  unsigned long long s[kStatsSlots];
   HIP_TRY(hipMemcpy(s, t->d_stats, sizeof(s), hipMemcpyDeviceToHost));
   o->rays = s[StatsCounters::kRays];
   o->paths = s[StatsCounters::kPaths];
@@ -655,7 +655,8 @@ int rt2_tracer_get_stats(rt2_tracer* t, rt2_stats* o) {
   o->medium_tests = s[StatsCounters::kMediumTests];
   o->list_visits = s[StatsCounters::kListVisits];
   o->overflow = s[StatsCounters::kCount];
-  for (int k = 0; k < 4; k++) o->stamps[k] = s[9 + k];
+  for (int k = 0; k < 4; k++) o->stamps[k] = s[StatsCounters::kStamps + k];
+  for (int k = 0; k < 8; k++) o->diag[k] = s[StatsCounters::kDiag + k];
   o->launches = t->launches;
   o->kernel_ms = t->kernel_ms;
   return RT2_OK;
@@ -665,7 +666,7 @@ int rt2_tracer_reset_stats(rt2_tracer* t) {
   if (!t) return Fail(RT2_ERR_INVALID, "null tracer");
   int rc = Sync(t);
   if (rc != RT2_OK) return rc;
-  HIP_TRY(hipMemset(t->d_stats, 0, 16 * sizeof(unsigned long long)));
+  HIP_TRY(hipMemset(t->d_stats, 0, kStatsSlots * sizeof(unsigned long long)));
   t->launches = 0;
   t->kernel_ms = 0;
   return RT2_OK;

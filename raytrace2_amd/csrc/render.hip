@@ -47,8 +47,11 @@ constexpr int kBlock = 256;
 #ifndef RT2_EXP_FAST_DIV
 #define RT2_EXP_FAST_DIV 0
 #endif
+#ifndef RT2_EXP_WAVESTEPS
+#define RT2_EXP_WAVESTEPS 0  // diagnostic build: per-wave linear-traversal step counts into diag slots
+#endif
 #ifndef RT2_EXP_STAMPS
-#define RT2_EXP_STAMPS 0  // diagnostic build: per-section s_memtime sums into stats slots 9..12
+#define RT2_EXP_STAMPS 0  // diagnostic build: per-section s_memtime sums into the stamp slots
 #endif
 #ifndef RT2_MIN_WAVES_PER_EU
 #define RT2_MIN_WAVES_PER_EU 1
@@ -156,14 +159,23 @@ __device__ __forceinline__ float uf(uint32_t u) { return __uint_as_float(u); }
 // of one per value: under divergence every refill site executes for the whole wave).
 __device__ __forceinline__ void philox(uint32_t k0, uint32_t k1, uint32_t pixel, uint32_t frame, uint32_t block,
                                        uint32_t& r0, uint32_t& r1, uint32_t& r2, uint32_t& r3) {
-  uint32_t c0 = pixel, c1 = frame, c2 = block, c3 = 0x52543250u, key0 = k0, key1 = k1;
+  uint32_t c0 = pixel, c1 = frame, c2 = block, c3 = 0x52543250u;
+  // The keys are wave-uniform: opaque here so the 20 round keys are recomputed with SALU adds at
+  // each call instead of being hoisted out of the render loop (and spilled to VGPR lanes).
+  uint32_t key0 = k0, key1 = k1;
+  asm volatile("" : "+s"(key0), "+s"(key1));
+  const uint32_t m0 = 0xD2511F53u, m1 = 0xCD9E8D57u;
 #pragma unroll
   for (int r = 0; r < (RT2_EXP_CHEAP_RNG ? 2 : 10); r++) {
-    uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
-    uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
-    c0 = hi1 ^ c1 ^ key0;
+    // one v_mad_u64_u32 gives both halves of each 32x32 product; xor3 is one v_bitop3_b32
+    uint64_t p0, p1;
+    asm("v_mad_u64_u32 %0, vcc, %1, %2, 0" : "=v"(p0) : "s"(m0), "v"(c0) : "vcc");
+    asm("v_mad_u64_u32 %0, vcc, %1, %2, 0" : "=v"(p1) : "s"(m1), "v"(c2) : "vcc");
+    const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(c0) : "v"(hi1), "v"(c1), "s"(key0));
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(c2) : "v"(hi0), "v"(c3), "s"(key1));
     c1 = lo1;
-    c2 = hi0 ^ c3 ^ key1;
     c3 = lo0;
     key0 += 0x9E3779B9u;
     key1 += 0xBB67AE85u;
@@ -242,7 +254,23 @@ __device__ __forceinline__ f3 refract(f3 uv, f3 n, float etai_over_etat) {
 
 struct Counters {
   uint32_t bvh, quad, sphere, xform, medium, list;
+#if RT2_EXP_WAVESTEPS
+  // wave-level (counted by the first active lane): trace calls, steps, bvh, quad pairs, single
+  // quads, xform, xform exits, active lanes at trace (summed by every lane)
+  uint32_t wd[8];
+#endif
 };
+#if RT2_EXP_WAVESTEPS
+#define RT2_WAVE(k)                                                           \
+  do {                                                                        \
+    if ((int)__lane_id() == __builtin_amdgcn_readfirstlane((int)__lane_id())) \
+      cnt.wd[k]++;                                                            \
+  } while (0)
+#else
+#define RT2_WAVE(k) \
+  do {              \
+  } while (0)
+#endif
 
 // ------------------------------------------------------------------------------------------
 // Primitive tests: return whether the primitive is hit inside the interval and its t.
@@ -594,6 +622,10 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
   uint32_t cur_xf = kRefNone;
   uint32_t next = 0;  // this lane's next step
   const uint32_t len = P.lin_len;
+  RT2_WAVE(0);
+#if RT2_EXP_WAVESTEPS
+  cnt.wd[7]++;
+#endif
   while (true) {
     // wave-uniform step = min over live lanes of `next`
     uint32_t i = __builtin_amdgcn_readfirstlane(next);
@@ -602,6 +634,18 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
     if (i >= len) break;
     const u32x4 st = sld4(prog, i * 16u);
     const uint32_t kind = st.x, off = st.z;
+    RT2_WAVE(1);
+    if (kind == kBvh) RT2_WAVE(2);
+    if (kind == kXform) RT2_WAVE(5);
+    if (kind == kXformExit) RT2_WAVE(6);
+    if (kind == kQuad) {
+#if RT2_EXP_WAVESTEPS
+      if ((int)__lane_id() == __builtin_amdgcn_readfirstlane((int)__lane_id())) {
+        cnt.wd[3] += st.w / 2u;
+        cnt.wd[4] += st.w & 1u;
+      }
+#endif
+    }
     if (next != i) continue;
     next = i + 1u;
     if (kind == kBvh) {
@@ -879,7 +923,7 @@ __global__ __launch_bounds__(kBlock, RT2_MIN_WAVES_PER_EU) void render_kernel(co
   f3 ro = mk(0, 0, 0), rd = mk(0, 0, 1), thr = mk(1, 1, 1);
   float rtime = 0.0f;
   int depth_left = 0;
-  Counters cnt = {0, 0, 0, 0, 0, 0};
+  Counters cnt = {};
   uint32_t rays = 0, paths = 0;
   bool overflow = false;
 
@@ -1041,10 +1085,10 @@ __global__ __launch_bounds__(kBlock, RT2_MIN_WAVES_PER_EU) void render_kernel(co
 
 #if RT2_EXP_STAMPS
   if (lane == __builtin_amdgcn_readfirstlane(lane)) {
-    atomicAdd(P.stats + 9, st_fetch);
-    atomicAdd(P.stats + 10, st_trace);
-    atomicAdd(P.stats + 11, st_shade);
-    atomicAdd(P.stats + 12, st_finish);
+    atomicAdd(P.stats + StatsCounters::kStamps, st_fetch);
+    atomicAdd(P.stats + StatsCounters::kStamps + 1, st_trace);
+    atomicAdd(P.stats + StatsCounters::kStamps + 2, st_shade);
+    atomicAdd(P.stats + StatsCounters::kStamps + 3, st_finish);
   }
 #endif
   atomicAdd(P.stats + StatsCounters::kRays, (unsigned long long)rays);
@@ -1058,6 +1102,9 @@ __global__ __launch_bounds__(kBlock, RT2_MIN_WAVES_PER_EU) void render_kernel(co
     atomicAdd(P.stats + StatsCounters::kListVisits, (unsigned long long)cnt.list);
   }
   if (overflow) atomicAdd(P.stats + StatsCounters::kCount, 1ull);  // overflow flag slot
+#if RT2_EXP_WAVESTEPS
+  for (int k = 0; k < 8; k++) atomicAdd(P.stats + StatsCounters::kDiag + k, (unsigned long long)cnt.wd[k]);
+#endif
 }
 
 // ------------------------------------------------------------------------------------------

@@ -102,7 +102,9 @@ struct CameraParams {
 
 struct StatsCounters {  // u64 slots written by the kernel
   enum { kRays = 0, kBvhTests, kQuadTests, kSphereTests, kXformVisits, kMediumTests, kListVisits, kPaths, kCount };
+  enum { kOverflow = kCount, kStamps = 9, kDiag = 16, kSlots = 32 };  // stamps / diag: diagnostic builds
 };
+constexpr int kStatsSlots = StatsCounters::kSlots;
 
 struct RenderParams {
   const void* nodes;      // float4[]

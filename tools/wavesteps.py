@@ -1,0 +1,30 @@
+"""Per-wave linear-traversal step counts (build with HIPFLAGS_EXTRA=-DRT2_EXP_WAVESTEPS=1; RT2_LIB=...).
+Prints, per ray cast, lane-level record tests and wave-level steps (a wave executes the union of the
+steps its lanes need)."""
+import json
+import sys
+
+import torch  # noqa: F401  (one HIP runtime)
+
+sys.path.insert(0, ".")
+import raytrace2_amd as R  # noqa: E402
+
+scene = sys.argv[1] if len(sys.argv) > 1 else "scenes/cornell_box_original.json"
+w, h, spp, frames = 1024, 1024, 1000, int(sys.argv[2]) if len(sys.argv) > 2 else 16
+sc = R.Scene(scene)
+tr = R.RayTracer(sc, 0)
+tr.SetSamplesPerPixel(spp)
+tr.enable_stats(True)
+tr.OnResize((w, h))
+tr.Render(frames)
+st = tr.stats()
+d = st["diag"]
+rays = st["rays"]
+wtrace = max(d[0], 1)
+out = {
+    "rays": rays, "lane_per_ray": {k: st[k] / rays for k in ("bvh_tests", "quad_tests", "xform_visits")},
+    "wave_trace_calls": d[0], "active_lanes_per_trace": d[7] / wtrace,
+    "wave_per_trace": {"steps": d[1] / wtrace, "bvh": d[2] / wtrace, "quad_pairs": d[3] / wtrace,
+                       "quad_single": d[4] / wtrace, "xform": d[5] / wtrace, "xform_exit": d[6] / wtrace},
+}
+print(json.dumps(out, indent=1))
