@@ -123,6 +123,7 @@ def _load():
         "rt2_tracer_get_stats": (i32, [vp, ctypes.POINTER(Stats)]),
         "rt2_tracer_reset_stats": (i32, [vp]),
         "rt2_write_image": (i32, [fp, i32, i32, ctypes.c_char_p, i32]),
+        "rt2_selftest": (i32, [i32, i32, u64, u64, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -139,3 +140,10 @@ def check(rc: int):
     if rc < 0:
         raise Rt2Error(rc, lib.rt2_last_error().decode(errors="replace"))
     return rc
+
+
+def selftest(which: int, n: int, seed: int = 1, device: int = 0):
+    """Kernel arithmetic self-test (rt2_selftest): returns (mismatches, inputs checked)."""
+    bad, checked = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    check(lib.rt2_selftest(device, which, n, seed, ctypes.byref(bad), ctypes.byref(checked)))
+    return bad.value, checked.value

@@ -15,6 +15,7 @@
 namespace rt2 {
 hipError_t LaunchRender(const RenderParams& p, int variant, bool stats, int grid, hipStream_t stream);
 int RenderBlocksPerCU(int variant, int mode, bool stats, size_t lds_bytes);
+hipError_t LaunchSelftest(int which, unsigned long long n, uint32_t seed, unsigned long long* d_out, hipStream_t stream);
 int RenderMode(const RenderParams& p);
 int RenderBlockSize();
 int RenderVariant(uint32_t features);
@@ -659,6 +660,25 @@ int rt2_tracer_get_stats(rt2_tracer* t, rt2_stats* o) {
   for (int k = 0; k < 8; k++) o->diag[k] = s[StatsCounters::kDiag + k];
   o->launches = t->launches;
   o->kernel_ms = t->kernel_ms;
+  return RT2_OK;
+}
+
+int rt2_selftest(int device, int which, uint64_t n, uint64_t seed, uint64_t* mismatches, uint64_t* checked) {
+  if (!mismatches || !checked) return Fail(RT2_ERR_INVALID, "null argument");
+  if (which < 0 || which > 1) return Fail(RT2_ERR_INVALID, "unknown self-test");
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return Fail(RT2_ERR_HIP, "no HIP device available");
+  HIP_TRY(hipSetDevice(device));
+  unsigned long long* d = nullptr;
+  HIP_TRY(hipMalloc(&d, 2 * sizeof(unsigned long long)));
+  unsigned long long h[2] = {0, 0};
+  hipError_t e = hipMemset(d, 0, sizeof(h));
+  if (e == hipSuccess) e = LaunchSelftest(which, (unsigned long long)n, (uint32_t)seed, d, nullptr);
+  if (e == hipSuccess) e = hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  if (e != hipSuccess) return HipFail(e, "self-test");
+  *mismatches = h[0];
+  *checked = h[1];
   return RT2_OK;
 }
 

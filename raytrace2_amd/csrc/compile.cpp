@@ -71,16 +71,23 @@ struct Flattener {
         uint32_t off = Alloc(kQuadRecords);
         Put(off, o.n.x, o.n.y, o.n.z, o.d);
         Put(off + 1, o.q.x, o.q.y, o.q.z, Bits(o.material));
-        // axis code k+1 when n and w have exact zeros off axis k (the kernel's exact axis-aligned test)
+        // axis code (the kernel's exact axis-aligned tests): k+1 when n and w have exact zeros off
+        // axis k; k+4 when in addition n[k] is exactly +-1 (then sign(n[k]) * D rides in w.w)
         uint32_t axis = 0;
+        float signed_d = 0.0f;
         for (int k = 0; k < 3 && !axis; k++) {
           int a = (k + 1) % 3, b = (k + 2) % 3;
-          if (o.n[a] == 0.0f && o.n[b] == 0.0f && o.w[a] == 0.0f && o.w[b] == 0.0f && o.n[k] != 0.0f)
+          if (o.n[a] == 0.0f && o.n[b] == 0.0f && o.w[a] == 0.0f && o.w[b] == 0.0f && o.n[k] != 0.0f) {
             axis = (uint32_t)k + 1;
+            if (o.n[k] == 1.0f || o.n[k] == -1.0f) {
+              axis = (uint32_t)k + 4;
+              signed_d = o.n[k] * o.d;  // exact
+            }
+          }
         }
         Put(off + 2, o.u.x, o.u.y, o.u.z, Bits(axis));
         Put(off + 3, o.v.x, o.v.y, o.v.z, 0);
-        Put(off + 4, o.w.x, o.w.y, o.w.z, 0);
+        Put(off + 4, o.w.x, o.w.y, o.w.z, signed_d);
         ref = make_ref(kQuad, off);
         out.quads++;
         break;
@@ -207,7 +214,7 @@ struct Flattener {
     for (size_t k = 0; k < kids.size(); k++) lind[4 * (off + 1 + k / 4) + k % 4] = Bits(kids[k]);
     return make_ref(kList, off);
   }
-  bool Linearize(int i, uint32_t parent_xf, std::vector<uint32_t>& lin, std::vector<float>& lind) {
+  bool Linearize(int i, uint32_t parent_xf, std::vector<uint32_t>& lin, std::vector<float>& lind, int xf_depth = 0) {
     if (lin.size() / 4 >= (size_t)kLinearMaxSteps) return false;
     const Obj& o = s.objs[(size_t)i];
     uint32_t src = ref_of.at(i) & kOffsetMask;
@@ -218,23 +225,25 @@ struct Flattener {
     switch (o.kind) {
       case kBvh: {
         size_t me = emit(kBvh, CopyRecords(src, kBvhRecords, lind), 0);
-        if (!Linearize(o.left, parent_xf, lin, lind)) return false;
+        if (!Linearize(o.left, parent_xf, lin, lind, xf_depth)) return false;
         if (!(o.left == o.right && !HasMedium(o.left))) {
-          if (!Linearize(o.right, parent_xf, lin, lind)) return false;
+          if (!Linearize(o.right, parent_xf, lin, lind, xf_depth)) return false;
         }
         lin[4 * me + 1] = (uint32_t)(lin.size() / 4);
         return true;
       }
       case kList:
         for (int c : o.children)
-          if (!Linearize(c, parent_xf, lin, lind)) return false;
+          if (!Linearize(c, parent_xf, lin, lind, xf_depth)) return false;
         return true;
       case kXform: {
         uint32_t off = CopyRecords(src, kXformRecords, lind);
         lind[4 * (off + 1) + 3] = Bits(parent_xf);
         uint32_t self = make_ref(kXform, off);
-        emit(kXform, off, 0);
-        if (!Linearize(o.child, self, lin, lind)) return false;
+        if (xf_depth >= kLinearMaxXformDepth) return false;  // the kernel nests one loop per level
+        size_t me = emit(kXform, off, 0);
+        if (!Linearize(o.child, self, lin, lind, xf_depth + 1)) return false;
+        lin[4 * me + 1] = (uint32_t)(lin.size() / 4);  // index of the matching exit step
         emit(kXformExit, off, parent_xf);
         return true;
       }
@@ -245,9 +254,12 @@ struct Flattener {
         emit(kMedium, off, 0);
         return lin.size() / 4 <= (size_t)kLinearMaxSteps;
       }
-      case kQuad:
-        emit(kQuad, CopyRecords(src, kQuadRecords, lind), 0);
+      case kQuad: {
+        uint32_t off = CopyRecords(src, kQuadRecords, lind);
+        lind[4 * (off + 3) + 3] = Bits(parent_xf);  // enclosing transform of this occurrence
+        emit(kQuad, off, 0);
         return lin.size() / 4 <= (size_t)kLinearMaxSteps;
+      }
       default:  // sphere
         emit(kSphere, CopyRecords(src, kSphereRecords, lind), 0);
         return lin.size() / 4 <= (size_t)kLinearMaxSteps;

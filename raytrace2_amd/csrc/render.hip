@@ -47,6 +47,15 @@ constexpr int kBlock = 256;
 #ifndef RT2_EXP_FAST_DIV
 #define RT2_EXP_FAST_DIV 0
 #endif
+#ifndef RT2_EXP_NO_FIN_AABB
+#define RT2_EXP_NO_FIN_AABB 0  // ablation: always the reference-order slab test
+#endif
+#ifndef RT2_EXP_NO_UNIT_QUAD
+#define RT2_EXP_NO_UNIT_QUAD 1  // unit-normal quads take the general axis-aligned test (measured faster: fewer SALU)
+#endif
+#ifndef RT2_EXP_TRACE_TWICE
+#define RT2_EXP_TRACE_TWICE 0  // cost probe: every ray is traced a second time (result discarded)
+#endif
 #ifndef RT2_EXP_WAVESTEPS
 #define RT2_EXP_WAVESTEPS 0  // diagnostic build: per-wave linear-traversal step counts into diag slots
 #endif
@@ -296,6 +305,32 @@ __device__ __forceinline__ bool aabb_hit(float4 lo, float4 hi, f3 o, f3 inv, flo
   return !(tmax <= tmin);
 }
 
+// aabb_hit when no slab value can be NaN (inv finite, so (bound - o) * inv is finite or +-inf):
+// the swap + glm::max/min chain with early exits then equals min/max of all axes at once.
+__device__ __forceinline__ bool aabb_hit_fin(float4 lo, float4 hi, f3 o, f3 inv, float tmin, float tmax) {
+  const float ax = (lo.x - o.x) * inv.x, bx = (hi.x - o.x) * inv.x;
+  const float ay = (lo.y - o.y) * inv.y, by = (hi.y - o.y) * inv.y;
+  const float az = (lo.z - o.z) * inv.z, bz = (hi.z - o.z) * inv.z;
+  const float t0 = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), tmin));
+  const float t1 = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), tmax));
+  return !(t1 <= t0);
+}
+__device__ __forceinline__ bool finite3(f3 v) {
+  return __builtin_isfinite(v.x) && __builtin_isfinite(v.y) && __builtin_isfinite(v.z);
+}
+
+// a / b, correctly rounded, from inv = fl(1 / b) (correctly rounded): q0 = a * inv is within
+// 2 ulp, one fma correction makes it faithful and a second one (Markstein) correctly rounded.
+// Equal to IEEE a / b whenever no intermediate under/overflows; the callers reject every case
+// where one could (|b| <= 1e-8 or a quotient below tmin). rt2_selftest checks it on the GPU.
+__device__ __forceinline__ float div_by_inv(float a, float b, float inv) {
+  float q = a * inv;
+  float r = fmaf(-b, q, a);
+  q = fmaf(r, inv, q);
+  r = fmaf(-b, q, a);
+  return fmaf(r, inv, q);
+}
+
 // Quad::Hit (Quad.cpp:19-43): inclusive interval (Contains)
 template <int kMode>
 __device__ __forceinline__ bool quad_t(const Nodes<kMode>& N, uint32_t off, f3 o, f3 d, float tmin, float tmax,
@@ -395,12 +430,37 @@ __device__ __forceinline__ bool quad_cand_aa(const float* w, f3 o, f3 d, float& 
   t_out = t;
   return !(fabsf(n_dot) <= 1e-8f) && (0.0f <= alpha && alpha <= 1.0f) && (0.0f <= beta && beta <= 1.0f);
 }
+// Unit-normal axis-aligned Quad::Hit (axis code K + 4, n[K] = s = +-1): n_dot = s * d[K] and
+// t = (D - s * o[K]) / (s * d[K]) = (sD - o[K]) / d[K] exactly (negation commutes with rounding),
+// computed from the ray's inv[K] = fl(1 / d[K]) with div_by_inv.
+template <int K>
+__device__ __forceinline__ bool quad_cand_unit(const float* w, f3 o, f3 d, f3 inv, float& t_out) {
+  constexpr int A = (K + 1) % 3, B = (K + 2) % 3;
+  const float wk = w[16 + K];
+  const float dk = comp<K>(d);
+  float t = div_by_inv(w[19] - comp<K>(o), dk, comp<K>(inv));
+  float pva = (comp<A>(o) + comp<A>(d) * t) - w[4 + A];
+  float pvb = (comp<B>(o) + comp<B>(d) * t) - w[4 + B];
+  float alpha = wk * (pva * w[12 + B] - w[12 + A] * pvb);  // w . cross(pv, v)
+  float beta = wk * (w[8 + A] * pvb - pva * w[8 + B]);    // w . cross(u, pv)
+  t_out = t;
+  return !(fabsf(dk) <= 1e-8f) && (0.0f <= alpha && alpha <= 1.0f) && (0.0f <= beta && beta <= 1.0f);
+}
 // quad candidate dispatched on a wave-uniform axis code
-__device__ __forceinline__ bool quad_cand_u(uint32_t axis, const float* w, f3 o, f3 d, float& t) {
+__device__ __forceinline__ bool quad_cand_u(uint32_t axis, const float* w, f3 o, f3 d, f3 inv, float& t) {
   switch (axis) {
     case 1: return quad_cand_aa<0>(w, o, d, t);
     case 2: return quad_cand_aa<1>(w, o, d, t);
     case 3: return quad_cand_aa<2>(w, o, d, t);
+#if RT2_EXP_NO_UNIT_QUAD
+    case 4: return quad_cand_aa<0>(w, o, d, t);
+    case 5: return quad_cand_aa<1>(w, o, d, t);
+    case 6: return quad_cand_aa<2>(w, o, d, t);
+#else
+    case 4: return quad_cand_unit<0>(w, o, d, inv, t);
+    case 5: return quad_cand_unit<1>(w, o, d, inv, t);
+    case 6: return quad_cand_unit<2>(w, o, d, inv, t);
+#endif
     default: return quad_cand_w(w, o, d, t);
   }
 }
@@ -616,6 +676,8 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
   f3 o = wo, d = wd;
   const f3 winv = mk(1.0f / wd.x, 1.0f / wd.y, 1.0f / wd.z);
   f3 inv = winv;
+  const bool wfin = finite3(winv);
+  bool fin = wfin;  // inv finite: the NaN-free slab test applies
   const float tmin = 0.001f;
   float tmax = FLT_MAX;
   bool any = false;
@@ -652,7 +714,12 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
       if (kStats) cnt.bvh++;
       const u32x8 b = sld8(recs, off * 16u);
       float4 lo = make_float4(uf(b[0]), uf(b[1]), uf(b[2]), 0.0f), hi = make_float4(uf(b[4]), uf(b[5]), uf(b[6]), 0.0f);
-      if (!aabb_hit(lo, hi, o, inv, tmin, tmax)) next = st.y;
+#if RT2_EXP_NO_FIN_AABB
+      const bool in = aabb_hit(lo, hi, o, inv, tmin, tmax);
+#else
+      const bool in = __all(fin) ? aabb_hit_fin(lo, hi, o, inv, tmin, tmax) : aabb_hit(lo, hi, o, inv, tmin, tmax);
+#endif
+      if (!in) next = st.y;
     } else if (kind == kQuad) {
       // a run of st.w quads with contiguous records: two candidates in flight, applied in order
       const uint32_t run = st.w;
@@ -673,8 +740,8 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
           for (int j = 0; j < 12; j++) w1[j] = uf(b2[4 + j]);
 #pragma unroll
           for (int j = 0; j < 8; j++) w1[12 + j] = uf(c[j]);
-          ok0 = quad_cand_u(a[11], w0, o, d, t0);
-          ok1 = quad_cand_u(b2[15], w1, o, d, t1);
+          ok0 = quad_cand_u(a[11], w0, o, d, inv, t0);
+          ok1 = quad_cand_u(b2[15], w1, o, d, inv, t1);
           if (kStats) cnt.quad += 2;
         } else {
           u32x16 a;
@@ -684,7 +751,7 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
           for (int j = 0; j < 16; j++) w0[j] = uf(a[j]);
 #pragma unroll
           for (int j = 0; j < 4; j++) w0[16 + j] = uf(b2[j]);
-          ok0 = quad_cand_u(a[11], w0, o, d, t0);
+          ok0 = quad_cand_u(a[11], w0, o, d, inv, t0);
           t1 = 0.0f;
           if (kStats) cnt.quad += 1;
         }
@@ -722,6 +789,7 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
       o = no;
       d = normalize(nd);
       inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+      fin = finite3(inv);
       cur_xf = make_ref(kXform, off);
     } else if (Has<F, kFeatXform>() && kind == kXformExit) {
       cur_xf = st.w;
@@ -729,9 +797,11 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
         o = wo;
         d = wd;
         inv = winv;
+        fin = wfin;
       } else {
         ray_in_space(N, cur_xf, wo, wd, o, d);
         inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+        fin = finite3(inv);
       }
     } else if (Has<F, kFeatMedium>() && kind == kMedium) {
       if (kStats) cnt.medium++;
@@ -987,6 +1057,16 @@ __global__ __launch_bounds__(kBlock, RT2_MIN_WAVES_PER_EU) void render_kernel(co
       bool hit;
       if constexpr (kMode == kModeLinear) {
         hit = trace_linear<F, kStats>(P, ro, rd, rtime, path, h, cnt);
+#if RT2_EXP_TRACE_TWICE
+        {
+          f3 ro2 = ro;
+          asm volatile("" : "+v"(ro2.x), "+v"(ro2.y), "+v"(ro2.z));
+          HitRef h2;
+          Path p2 = path;
+          bool hit2 = trace_linear<F, kStats>(P, ro2, rd, rtime, p2, h2, cnt);
+          asm volatile("" ::"v"(h2.t), "v"(h2.prim), "v"(h2.xf), "v"((int)hit2));
+        }
+#endif
       } else {
         hit = trace_stack<F, kMode, kStats>(P, N, ro, rd, rtime, path, h, stk, cnt, overflow);
       }
@@ -1144,6 +1224,48 @@ KernelFn Kernel(int v, int mode, bool stats) {
   return nullptr;
 }
 
+// ------------------------------------------------------------------------------------------
+// Self-tests of the kernel's exact shortcuts on random inputs (rt2_selftest):
+//   which 0: div_by_inv(a, b, fl(1/b)) == a / b for |b| > 1e-8, |a / b| >= 1e-3 (accepted quad t)
+//   which 1: aabb_hit_fin == aabb_hit for rays with finite inv
+__device__ __forceinline__ float rand_float(uint32_t bits, int emin, int emax, uint32_t sel) {
+  const int e = emin + (int)(sel % (uint32_t)(emax - emin + 1));
+  return __uint_as_float((bits & 0x807FFFFFu) | ((uint32_t)(e + 127) << 23));
+}
+__global__ void selftest_kernel(int which, unsigned long long n, uint32_t seed, unsigned long long* out) {
+  unsigned long long bad = 0, checked = 0;
+  for (unsigned long long idx = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; idx < n;
+       idx += (unsigned long long)gridDim.x * blockDim.x) {
+    uint32_t r0, r1, r2, r3;
+    philox(seed, 0x7E57u, (uint32_t)idx, (uint32_t)(idx >> 32), 0u, r0, r1, r2, r3);
+    if (which == 0) {
+      const float a = rand_float(r0, -30, 17, r2 & 0xFFFFu);
+      const float b = rand_float(r1, -27, 1, r2 >> 16);
+      const float q = a / b;
+      if (!(fabsf(b) > 1e-8f) || !(fabsf(q) >= 1e-3f) || !__builtin_isfinite(q)) continue;
+      checked++;
+      const float inv = 1.0f / b;
+      if (__float_as_uint(div_by_inv(a, b, inv)) != __float_as_uint(q)) bad++;
+    } else {
+      uint32_t s0, s1, s2, s3;
+      philox(seed, 0xAABBu, (uint32_t)idx, (uint32_t)(idx >> 32), 1u, s0, s1, s2, s3);
+      const float lo_x = rand_float(r0, -4, 9, r1), hi_x = lo_x + rand_float(r1, -6, 8, r0 >> 7);
+      const float lo_y = rand_float(r2, -4, 9, r3), hi_y = lo_y + rand_float(r3, -6, 8, r2 >> 7);
+      const float lo_z = rand_float(s0, -4, 9, s1), hi_z = lo_z + rand_float(s1, -6, 8, s0 >> 7);
+      const f3 o = mk(rand_float(s2, -3, 10, s3), rand_float(s3, -3, 10, s2 >> 5), rand_float(s2 ^ s3, -3, 10, s1));
+      const f3 d = mk(rand_float(r0 ^ s0, -40, 1, r3), rand_float(r1 ^ s1, -40, 1, s3 >> 3), rand_float(r2 ^ s2, -40, 1, r0));
+      const f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+      if (!finite3(inv)) continue;
+      const float tmax = (s3 & 1u) ? FLT_MAX : rand_float(s0 ^ r3, -3, 12, s2);
+      const float4 lo = make_float4(lo_x, lo_y, lo_z, 0.0f), hi = make_float4(hi_x, hi_y, hi_z, 0.0f);
+      checked++;
+      if (aabb_hit_fin(lo, hi, o, inv, 0.001f, tmax) != aabb_hit(lo, hi, o, inv, 0.001f, tmax)) bad++;
+    }
+  }
+  atomicAdd(out, bad);
+  atomicAdd(out + 1, checked);
+}
+
 }  // namespace dev
 
 int RenderVariant(uint32_t features) {
@@ -1173,6 +1295,11 @@ hipError_t LaunchRender(const RenderParams& p, int variant, bool stats, int grid
   dev::KernelFn fn = dev::Kernel(variant, RenderMode(p), stats);
   if (!fn) return hipErrorInvalidValue;
   hipLaunchKernelGGL(fn, dim3(grid), dim3(dev::kBlock), RenderLdsBytes(p), stream, p);
+  return hipGetLastError();
+}
+
+hipError_t LaunchSelftest(int which, unsigned long long n, uint32_t seed, unsigned long long* d_out, hipStream_t stream) {
+  hipLaunchKernelGGL(dev::selftest_kernel, dim3(4096), dim3(256), 0, stream, which, n, seed, d_out);
   return hipGetLastError();
 }
 

@@ -33,8 +33,10 @@ inline constexpr uint32_t make_ref(uint32_t kind, uint32_t off) { return (kind <
 // Record layouts (each line one float4; "(bits)" = uint32 stored with __float_as_uint):
 //  BVH   : (min.xyz, left_ref bits) (max.xyz, right_ref bits)  right_ref = kRefNone when a
 //          span-1 leaf's duplicate test is provably a no-op (no medium below it).
-//  QUAD  : (n.xyz, D) (q.xyz, material bits) (u.xyz, axis bits) (v.xyz, 0) (w.xyz, 0)
-//          axis = k + 1 when n and w are exactly zero off axis k (exact axis-aligned test), else 0
+//  QUAD  : (n.xyz, D) (q.xyz, material bits) (u.xyz, axis bits) (v.xyz, 0) (w.xyz, sD)
+//          axis = k + 1 when n and w are exactly zero off axis k (exact axis-aligned test),
+//          k + 4 when moreover n[k] = s = +-1 exactly (sD = s * D), else 0
+//          In the threaded program's record copy (lind), v.w = the enclosing XFORM's lind ref.
 //  SPHERE: (c0.xyz, radius) (displacement.xyz, material bits)
 //  LIST  : (count bits, flags bits, 0, 0) then child refs, 4 per record. flags bit0 = every
 //          child is a QUAD or SPHERE (iterated inline, no stack traffic).
@@ -82,14 +84,16 @@ constexpr int kLdsSceneBytesMax = 96 * 1024;  // scenes up to this size are stag
 //   kind kQuad / kSphere / kMedium: record of the primitive; the next step is always index + 1;
 //     for kQuad, aux = length of the run of consecutive quads starting here with no skip target
 //     inside it (tested as a batch: the candidate math of two quads is interleaved)
-//   kind kXform: enter the transform (record = XFORM record); kXformExit: leave it
-//     (record = XFORM record, aux = parent XFORM ref or kRefNone)
+//   kind kXform: enter the transform (record = XFORM record, skip = index of its kXformExit);
+//     the kernel walks the steps up to the exit in a nested loop with the transformed ray
+//   kind kXformExit: leave it (record = XFORM record, aux = parent XFORM ref or kRefNone)
 // Lists vanish (their children follow each other); span-1 leaves with a medium appear twice.
 // Record offsets refer to a separate record stream (RenderParams::lind) holding each step's
 // record in program order, so a run of quads is contiguous.
 // All lanes of a wave walk this array in lockstep at the smallest pending index, so the step
 // kind is wave-uniform and its record is read with scalar loads.
 constexpr int kLinearMaxSteps = 1024;  // scenes whose program is longer use the stack traversal
+constexpr int kLinearMaxXformDepth = 8;  // deeper transform nesting uses the stack traversal
 
 enum TraversalMode : int { kModeStackGlobal = 0, kModeStackLds = 1, kModeLinear = 2 };
 

@@ -1,0 +1,19 @@
+"""The kernel's exact arithmetic shortcuts against their reference form on the GPU (rt2_selftest).
+
+* div_by_inv: the unit-normal axis-aligned quad test divides by the ray's correctly rounded
+  reciprocal with two fma corrections; it must equal IEEE a / b bit for bit wherever the quad test
+  can accept the quotient (|b| > 1e-8, a / b >= tmin).
+* aabb_hit_fin: the NaN-free slab test must decide exactly like the reference's swap +
+  glm::max/min chain with early exits (AABB.hpp:34-47) for every ray with a finite inverse.
+"""
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("which,n", [(0, 1 << 28), (1, 1 << 26)], ids=["div_by_inv", "aabb_fin"])
+def test_selftest(have_gpu, which, n):
+    from raytrace2_amd._native import selftest
+    bad, checked = selftest(which, n, seed=20241015)
+    assert checked > n // 4
+    assert bad == 0, f"{bad} of {checked} differ"
