@@ -43,6 +43,7 @@ RT2_API const char* rt2_version(void);
  * to <scene dir>/<name>.json. `seed` keys the Perlin-table random streams (the reference draws them
  * from its unseeded RNG at load, PerlinNoiseGen.cpp:41-50). */
 RT2_API int rt2_scene_load(const char* path, uint64_t seed, rt2_scene** out);
+/* The environment variable RT2_NO_LIST_ACCEL=1 at load keeps every list a linear child loop. */
 RT2_API void rt2_scene_free(rt2_scene* scene);
 
 typedef struct {
@@ -53,6 +54,8 @@ typedef struct {
   int bvh_nodes, quads, spheres, lists, xforms, media; /* flattened records */
   int max_stack, bvh_depth;
   uint64_t node_bytes;
+  int acc_lists, acc_nodes; /* sphere lists given an exact acceleration tree, and its nodes */
+  int linear_steps;         /* threaded-program length (0: the scene uses the stack traversal) */
 } rt2_scene_info;
 RT2_API int rt2_scene_get_info(const rt2_scene* scene, rt2_scene_info* out);
 /* Material table, 8 floats per material: type, albedo.xyz, fuzz, refraction_index, tex_idx, 0.

@@ -189,7 +189,9 @@ int rt2_scene_load(const char* path, uint64_t seed, rt2_scene** out) {
     bool io = err.rfind("Failed to open", 0) == 0;
     return Fail(io ? RT2_ERR_IO : RT2_ERR_SCENE, err);
   }
-  if (!CompileScene(s->scene, s->compiled, err)) return Fail(RT2_ERR_SCENE, err);
+  const char* na = getenv("RT2_NO_LIST_ACCEL");
+  const bool accel = !(na && na[0] == '1');
+  if (!CompileScene(s->scene, s->compiled, err, accel)) return Fail(RT2_ERR_SCENE, err);
   *out = s.release();
   return RT2_OK;
 }
@@ -217,6 +219,9 @@ int rt2_scene_get_info(const rt2_scene* s, rt2_scene_info* o) {
   o->max_stack = c.max_stack;
   o->bvh_depth = c.bvh_depth;
   o->node_bytes = (uint64_t)c.nodes.size() * sizeof(float);
+  o->acc_lists = c.acc_lists;
+  o->acc_nodes = c.acc_nodes;
+  o->linear_steps = (int)(c.lin.size() / 4);
   return RT2_OK;
 }
 

@@ -1,5 +1,8 @@
 // compile.cpp — flattens the host object graph (scene.h) into the node array the gfx950 kernel
 // walks (rt2_layout.h), and proves the kernel's traversal-stack bound for the scene.
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
 #include <cstring>
 #include <functional>
 #include <unordered_map>
@@ -14,6 +17,8 @@ struct Flattener {
   const Scene& s;
   CompiledScene& out;
   std::unordered_map<int, uint32_t> ref_of;  // obj index -> node ref (DAG sharing)
+  std::unordered_map<int, int> acc_depth;    // accelerated list obj -> tree depth
+  bool accelerate_lists = true;
   std::unordered_map<int, bool> medium_memo;
 
   Flattener(const Scene& sc, CompiledScene& o) : s(sc), out(o) {}
@@ -53,6 +58,79 @@ struct Flattener {
     }
     medium_memo[i] = r;
     return r;
+  }
+
+  // A leaf-only list of spheres, long enough, whose children's records are distinct and in list
+  // order (so record-offset order is child order; the kernel breaks equal roots by it).
+  bool AccelEligible(const Obj& o, const std::vector<uint32_t>& refs) const {
+    if ((int)refs.size() < kListAccelMin) return false;
+    for (size_t k = 0; k < refs.size(); k++) {
+      if ((refs[k] >> 28) != kSphere) return false;
+      if (k && (refs[k] & kOffsetMask) <= (refs[k - 1] & kOffsetMask)) return false;
+    }
+    for (int c : o.children)
+      if (s.objs[(size_t)c].radius <= 0.0f) return false;
+    return true;
+  }
+  // Median-split tree over the children's boxes; returns the subtree ref and its depth.
+  uint32_t BuildAcc(std::vector<std::pair<int, uint32_t>>& items, size_t lo, size_t hi, int& depth) {
+    if (hi - lo == 1) {
+      depth = 0;
+      return make_ref(kAccSphere, items[lo].second & kOffsetMask);
+    }
+    AABB box = s.objs[(size_t)items[lo].first].aabb;
+    vec3 cmin(FLT_MAX, FLT_MAX, FLT_MAX), cmax(-FLT_MAX, -FLT_MAX, -FLT_MAX);
+    for (size_t k = lo; k < hi; k++) {
+      const AABB& b = s.objs[(size_t)items[k].first].aabb;
+      box = AABB(box, b);
+      vec3 c((b.x.min + b.x.max) * 0.5f, (b.y.min + b.y.max) * 0.5f, (b.z.min + b.z.max) * 0.5f);
+      cmin = vec3(std::min(cmin.x, c.x), std::min(cmin.y, c.y), std::min(cmin.z, c.z));
+      cmax = vec3(std::max(cmax.x, c.x), std::max(cmax.y, c.y), std::max(cmax.z, c.z));
+    }
+    vec3 ext = cmax - cmin;
+    int axis = ext.x >= ext.y && ext.x >= ext.z ? 0 : (ext.y >= ext.z ? 1 : 2);
+    auto key = [&](const std::pair<int, uint32_t>& it) {
+      const AABB& b = s.objs[(size_t)it.first].aabb;
+      const Interval& iv = axis == 0 ? b.x : (axis == 1 ? b.y : b.z);
+      return iv.min + iv.max;
+    };
+    size_t mid = lo + (hi - lo) / 2;
+    std::nth_element(items.begin() + (long)lo, items.begin() + (long)mid, items.begin() + (long)hi,
+                     [&](const auto& a, const auto& b) { return key(a) < key(b) || (key(a) == key(b) && a.second < b.second); });
+    int dl = 0, dr = 0;
+    uint32_t l = BuildAcc(items, lo, mid, dl);
+    uint32_t r = BuildAcc(items, mid, hi, dr);
+    depth = 1 + std::max(dl, dr);
+    uint32_t off = Alloc(kBvhRecords);
+    Put(off, box.x.min, box.y.min, box.z.min, Bits(l));
+    Put(off + 1, box.x.max, box.y.max, box.z.max, Bits(r));
+    out.acc_nodes++;
+    return make_ref(kAccBvh + (uint32_t)axis, off);
+  }
+  uint32_t EmitListAcc(int i, const Obj& o, const std::vector<uint32_t>& refs) {
+    std::vector<std::pair<int, uint32_t>> items;
+    float rmin = FLT_MAX;
+    AABB box = s.objs[(size_t)o.children[0]].aabb;
+    for (size_t k = 0; k < refs.size(); k++) {
+      const Obj& c = s.objs[(size_t)o.children[k]];
+      items.emplace_back(o.children[k], refs[k]);
+      rmin = std::min(rmin, c.radius);
+      box = AABB(box, c.aabb);
+    }
+    int depth = 0;
+    uint32_t root = BuildAcc(items, 0, items.size(), depth);
+    acc_depth[i] = depth;
+    vec3 c((box.x.min + box.x.max) * 0.5f, (box.y.min + box.y.max) * 0.5f, (box.z.min + box.z.max) * 0.5f);
+    float hx = box.x.max - c.x, hy = box.y.max - c.y, hz = box.z.max - c.z;
+    float R = std::sqrt(hx * hx + hy * hy + hz * hz) * 1.001f + 1e-3f;
+    uint32_t off = Alloc(2);
+    // pad(L) = (k2 L + k1) L + k0: k2 = 4e-6 / r_min bounds the discriminant's float error
+    // (~1e-6 a|oc|^2) turned into distance beyond the radius, with a 4x margin; k1, k0 cover the
+    // rounding of roots and of the slab test
+    Put(off, c.x, c.y, c.z, R);
+    Put(off + 1, 4e-6f / rmin, 1e-5f, 1e-4f, Bits(root));
+    out.acc_lists++;
+    return make_ref(kListAcc, off);
   }
 
   bool IsLeafPrim(int i) const {
@@ -108,6 +186,11 @@ struct Flattener {
           if (r == kRefNone) return kRefNone;
           refs.push_back(r);
           leaf_only = leaf_only && IsLeafPrim(c);
+        }
+        if (accelerate_lists && AccelEligible(o, refs)) {
+          ref = EmitListAcc(i, o, refs);
+          out.lists++;
+          break;
         }
         int recs = 1 + (int)((refs.size() + 3) / 4);
         uint32_t off = Alloc(recs);
@@ -233,6 +316,7 @@ struct Flattener {
         return true;
       }
       case kList:
+        if (acc_depth.count(i)) return false;  // accelerated lists use the stack traversal
         for (int c : o.children)
           if (!Linearize(c, parent_xf, lin, lind, xf_depth)) return false;
         return true;
@@ -279,6 +363,8 @@ struct Flattener {
         return std::max(2, std::max(1 + nl, nr));
       }
       case kList: {
+        auto acc = acc_depth.find(i);
+        if (acc != acc_depth.end()) return acc->second;  // one pushed sibling per tree level
         bool leaf_only = true;
         for (int c : o.children) leaf_only = leaf_only && IsLeafPrim(c);
         if (leaf_only) return 0;
@@ -348,13 +434,14 @@ void PackTextures(const Scene& s, CompiledScene& out) {
 
 }  // namespace
 
-bool CompileScene(const Scene& s, CompiledScene& out, std::string& err) {
+bool CompileScene(const Scene& s, CompiledScene& out, std::string& err, bool accelerate_lists) {
   out = CompiledScene();
   if (s.root < 0) {
     err = "scene has no BVH root";
     return false;
   }
   Flattener fl(s, out);
+  fl.accelerate_lists = accelerate_lists;
   out.root = fl.Emit(s.root, kRefNone, err);
   if (out.root == kRefNone) return false;
   int depth = 0;

@@ -578,6 +578,8 @@ __device__ __forceinline__ bool trace_stack(const RenderParams& P, const Nodes<k
   int sp = 0;
   uint32_t lword = 0, lrem = 0;  // leaf-list cursor: next child-ref word, children left
   uint32_t cur = P.root;         // next step
+  float acc_pad = 0.0f;          // accelerated list: this ray's box padding
+  uint32_t acc_best = kRefNone;  // accelerated list: record of its current closest child
   while (cur != kRefNone) {
     uint32_t kind = cur >> 28, off = cur & kOffsetMask;
     if (kind == kQuad || (Has<F, kFeatSphere>() && kind == kSphere)) {
@@ -646,6 +648,51 @@ __device__ __forceinline__ bool trace_stack(const RenderParams& P, const Nodes<k
         any = true;
         h.prim = cur;
         h.xf = cur_xf;
+      }
+    } else if (Has<F, kFeatSphere>() && kind == kListAcc) {
+      // HittableList::Hit over many spheres through its exact acceleration tree (rt2_layout.h)
+      if (kStats) cnt.list++;
+      const float4 r0 = N[off], r1 = N[off + 1];
+      const f3 dc = o - xyz(r0);
+      const float L = sqrtf(dot(dc, dc)) * 1.0001f + r0.w;
+      acc_pad = (r1.x * L + r1.y) * L + r1.z;
+      acc_best = kRefNone;
+      cur = bits(r1.w);
+      continue;
+    } else if (Has<F, kFeatSphere>() && is_acc_bvh(kind)) {
+      if (kStats) cnt.bvh++;
+      const float4 lo = N[off], hi = N[off + 1];
+      // padded slab test; NaN from 0 * inf is ignored by fminf/fmaxf (a ray in a padded face
+      // plane with zero direction component stays >= pad away from every child)
+      const float ax = ((lo.x - acc_pad) - o.x) * inv.x, bx = ((hi.x + acc_pad) - o.x) * inv.x;
+      const float ay = ((lo.y - acc_pad) - o.y) * inv.y, by = ((hi.y + acc_pad) - o.y) * inv.y;
+      const float az = ((lo.z - acc_pad) - o.z) * inv.z, bz = ((hi.z + acc_pad) - o.z) * inv.z;
+      const float t0 = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), tmin));
+      const float t1 = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), tmax));
+      if (t0 <= t1) {
+        const uint32_t axis = kind - kAccBvh;
+        const float dax = axis == 0u ? d.x : (axis == 1u ? d.y : d.z);
+        const uint32_t nr = bits(lo.w), fr = bits(hi.w);
+        const bool flip = dax < 0.0f;  // visit the child nearer along the split axis first
+        if (sp + 1 > cap) {
+          overflow = true;
+        } else {
+          stk[(sp++) * kBlock] = flip ? nr : fr;
+        }
+        cur = flip ? fr : nr;
+        continue;
+      }
+    } else if (Has<F, kFeatSphere>() && kind == kAccSphere) {
+      // smallest root wins; an equal root goes to the lower child index = lower record offset
+      if (kStats) cnt.sphere++;
+      float t;
+      if (sphere_t(N, off, o, d, time, tmin, FLT_MAX, t) &&
+          (t < tmax || (t == tmax && acc_best != kRefNone && off < acc_best))) {
+        tmax = t;
+        any = true;
+        h.prim = make_ref(kSphere, off);
+        h.xf = cur_xf;
+        acc_best = off;
       }
     }
     // next step: the leaf-list cursor first, then the stack

@@ -24,7 +24,12 @@ enum NodeKind : uint32_t {
   kXform = 4,
   kMedium = 5,
   kXformExit = 6,  // traversal-stack marker only (never stored in the node array)
+  kListAcc = 7,    // a large leaf-only sphere list with its exact acceleration tree
+  kAccBvh = 8,     // 8 + split axis (8, 9, 10): node of a list's acceleration tree
+  kAccSphere = 11, // a sphere reached through a list's acceleration tree
 };
+inline constexpr bool is_acc_bvh(uint32_t kind) { return kind - kAccBvh < 3u; }
+constexpr int kListAccelMin = 32;  // leaf-only sphere lists at least this long get a tree
 
 constexpr uint32_t kRefNone = 0xFFFFFFFFu;
 constexpr uint32_t kOffsetMask = 0x0FFFFFFFu;
@@ -43,6 +48,18 @@ inline constexpr uint32_t make_ref(uint32_t kind, uint32_t off) { return (kind <
 //  XFORM : (invM col0.xyz, child_ref bits) (invM col1.xyz, parent_xform_ref bits)
 //          (invM col2.xyz, 0) (invM col3.xyz, 0) (M col0.xyz,0) (M col1.xyz,0) (M col2.xyz,0) (M col3.xyz,0)
 //  MEDIUM: (neg_inv_density, material bits, boundary_ref bits, 0)
+//  LISTACC: (center.xyz, R) (k2, k1, k0, root_ref bits): a HittableList of n >= kListAccelMin
+//          spheres (HittableList.cpp:8-22). The list returns the smallest accepted root and, on
+//          equal roots, its first child (Sphere uses the strict Surrounds), so any visiting
+//          order gives the same hit when candidates are never wrongly culled and ties go to the
+//          lowest child index; the children's records are emitted in list order, so the index
+//          order is the record-offset order. The tree's boxes are padded per ray by
+//          pad = (k2 * L + k1) * L + k0, L = |o - center| + R (a bound on |center_i - o|), which
+//          covers the float error of Sphere::Hit's discriminant for rays that far away
+//          ("Exact list acceleration").
+//  ACCBVH: (min.xyz, near_ref bits) (max.xyz, far_ref bits); near = the child with the smaller
+//          centroids along the node's split axis (kind - kAccBvh); children are ACCBVH or
+//          ACCSPHERE refs (an ACCSPHERE ref points at the child's SPHERE record)
 constexpr uint32_t kListLeafOnly = 1u;
 
 constexpr int kBvhRecords = 2, kQuadRecords = 5, kSphereRecords = 2, kXformRecords = 8, kMediumRecords = 1;

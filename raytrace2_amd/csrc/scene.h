@@ -141,12 +141,14 @@ struct CompiledScene {
   std::vector<int> perlin_perm;
   int max_stack = 0;              // proven traversal-stack bound (entries)
   int bvh_nodes = 0, quads = 0, spheres = 0, lists = 0, xforms = 0, media = 0;
+  int acc_lists = 0, acc_nodes = 0;  // exact list acceleration trees (rt2_layout.h LISTACC)
   int bvh_depth = 0;
   uint32_t features = 0;          // rt2_layout.h Feature bits (defocus is added per render)
   std::vector<uint32_t> lin;      // threaded traversal program (4 words per step), empty if too long
   std::vector<float> lind;        // records of the program's steps, in program order (float4)
 };
-bool CompileScene(const Scene& s, CompiledScene& out, std::string& err);
+// accelerate_lists = false keeps every list a linear child loop (the reference's own order).
+bool CompileScene(const Scene& s, CompiledScene& out, std::string& err, bool accelerate_lists = true);
 
 // Philox4x32-10 (shared constants with the kernel; see render.hip)
 void Philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1);

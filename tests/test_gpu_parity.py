@@ -118,3 +118,19 @@ def test_every_traversal_mode_matches(have_gpu, monkeypatch, mode, name, w, h, s
     assert st["overflow"] == 0
     np.testing.assert_array_equal(rc, o_rc)
     assert np.array_equal(acc.view(np.uint32), o_acc.view(np.uint32))
+
+
+def test_list_acceleration_matches_linear_child_loop(have_gpu, monkeypatch):
+    """Book 2's 1000-sphere HittableList (HittableList.cpp:8-22) through its exact acceleration tree
+    gives bit-identical renders and ray counts to the reference's linear child loop, with far
+    fewer sphere tests."""
+    name, w, h, spp, frames = "book2_final_scene_10000_samples", 200, 200, 10000, 4
+    a1, r1, s1, _ = gpu_render(name, w, h, spp, frames, stats=True)
+    monkeypatch.setenv("RT2_NO_LIST_ACCEL", "1")
+    a2, r2, s2, _ = gpu_render(name, w, h, spp, frames, stats=True)
+    assert s1["overflow"] == 0 and s2["overflow"] == 0
+    np.testing.assert_array_equal(r1, r2)
+    assert s1["rays"] == s2["rays"]
+    mism = np.count_nonzero(a1.view(np.uint32) != a2.view(np.uint32))
+    assert mism == 0, f"{mism} floats differ"
+    assert s1["sphere_tests"] * 5 < s2["sphere_tests"], (s1["sphere_tests"], s2["sphere_tests"])
