@@ -19,7 +19,8 @@
 //  * log() in ConstantMedium and sin() in the marble texture are evaluated in double and
 //    rounded once (the reference calls glibc logf/sinf; difference <= 1 ulp).
 //  * pow(1-cos, 5) in Schlick is an explicit double multiplication chain (reference: std::pow).
-//  * RandInUnitDisk draws x before y (the reference's vec3(...) argument order is unspecified).
+//  * RandUnitVec3 / RandInUnitDisk draw their (identical) distributions by inverse-CDF maps
+//    instead of rejection loops, with a shared polynomial sin/cos (see CosSin2Pi).
 //  * Missing "rotation" in a transform is the identity quaternion (reference: uninitialised
 //    glm::quat, undefined behaviour; Serialize.cpp:114).
 // Compile with -ffp-contract=off: every float op below is rounded individually, like the
@@ -234,22 +235,47 @@ inline vec3 RandVec3(Rng& g, float min, float max) {
   float z = g.RandReal(min, max);
   return {x, y, z};
 }
-inline vec3 RandInUnitSphere(Rng& g) {
-  while (true) {
-    vec3 p = RandVec3(g, -1, 1);
-    float length_sq = dot(p, p);
-    if (1e-160 < (double)length_sq && length_sq <= 1.0) return p;
+// (cos 2 pi v, sin 2 pi v) for v in [0, 1): quarter turn by the exact split 4v = q + x, then
+// degree-9 odd / degree-8 even polynomials in x (max error 2e-7). The kernel evaluates the same
+// operations in the same order (render.hip cos_sin_2pi), so both round identically.
+inline void CosSin2Pi(float v, float& c, float& s) {
+  const float t = v * 4.0f;
+  const int q = (int)t;
+  const float x = t - (float)q;
+  const float x2 = x * x;
+  const float sp = ((((1.509560242993757e-4f * x2 + -4.672547802329063e-3f) * x2 + 7.968873530626297e-2f) * x2 +
+                     -6.459634304046631e-1f) * x2 + 1.570796251296997f) * x;
+  const float cp = (((8.59465915709734e-4f * x2 + -2.0813362672924995e-2f) * x2 + 2.536526620388031e-1f) * x2 +
+                    -1.2336987257003784f) * x2 + 1.0f;
+  switch (q) {
+    case 0: c = cp; s = sp; break;
+    case 1: c = -sp; s = cp; break;
+    case 2: c = -cp; s = -sp; break;
+    default: c = sp; s = -cp; break;
   }
+}
+// Math.hpp:26-43 draw RandUnitVec3 = normalize(RandInUnitSphere()) by rejection in [-1,1]^3 and
+// RandInUnitDisk by rejection in [-1,1]^2. The same distributions (uniform on the unit sphere /
+// in the unit disk) are drawn here by the inverse-CDF maps, two uniforms each and no retry loop
+// (a rejection loop costs a GPU wave its unluckiest lane's retries): z = 1 - 2u, phi = 2 pi v;
+// r = sqrt(u), phi = 2 pi v.
+inline vec3 RandUnitVec3(Rng& g) {
+  const float u = g.RandReal();
+  const float v = g.RandReal();
+  const float z = 1.0f - 2.0f * u;
+  const float r = std::sqrt(1.0f - z * z);
+  float c, s;
+  CosSin2Pi(v, c, s);
+  return {r * c, r * s, z};
 }
 inline vec3 RandInUnitDisk(Rng& g) {
-  while (true) {
-    float x = g.RandReal(-1, 1);
-    float y = g.RandReal(-1, 1);
-    vec3 p{x, y, 0};
-    if (dot(p, p) < 1.0) return p;
-  }
+  const float u = g.RandReal();
+  const float v = g.RandReal();
+  const float r = std::sqrt(u);
+  float c, s;
+  CosSin2Pi(v, c, s);
+  return {r * c, r * s, 0.0f};
 }
-inline vec3 RandUnitVec3(Rng& g) { return normalize(RandInUnitSphere(g)); }
 // Math.hpp:61-73
 inline bool NearZero(vec3 v) {
   constexpr double kEpsilon = 1e-8;

@@ -56,6 +56,9 @@ constexpr int kBlock = 256;
 #ifndef RT2_EXP_TRACE_TWICE
 #define RT2_EXP_TRACE_TWICE 0  // cost probe: every ray is traced a second time (result discarded)
 #endif
+#ifndef RT2_EXP_TWICE
+#define RT2_EXP_TWICE 0  // cost probes (bits): 1 resolve_hit, 2 rand_unit_vec3, 4 camera_ray run twice
+#endif
 #ifndef RT2_EXP_WAVESTEPS
 #define RT2_EXP_WAVESTEPS 0  // diagnostic build: per-wave linear-traversal step counts into diag slots
 #endif
@@ -237,17 +240,33 @@ struct Path {
 // Math.hpp:15 RandReal(min, max) = min + RandReal() * (max - min)
 __device__ __forceinline__ float rand_range(float u, float mn, float mx) { return mn + u * (mx - mn); }
 
-// Math.hpp:26-43: RandUnitVec3 = normalize(RandInUnitSphere()), one refill site per attempt
+// (cos 2 pi v, sin 2 pi v), v in [0, 1): exact quarter-turn split 4v = q + x and polynomials in x;
+// the oracle's CosSin2Pi evaluates the same operations in the same order.
+__device__ __forceinline__ void cos_sin_2pi(float v, float& c, float& s) {
+  const float t = v * 4.0f;
+  const int q = (int)t;
+  const float x = t - (float)q;
+  const float x2 = x * x;
+  const float sp = ((((1.509560242993757e-4f * x2 + -4.672547802329063e-3f) * x2 + 7.968873530626297e-2f) * x2 +
+                     -6.459634304046631e-1f) * x2 + 1.570796251296997f) * x;
+  const float cp = (((8.59465915709734e-4f * x2 + -2.0813362672924995e-2f) * x2 + 2.536526620388031e-1f) * x2 +
+                    -1.2336987257003784f) * x2 + 1.0f;
+  const bool odd = (q & 1) != 0, neg_c = q == 1 || q == 2, neg_s = q >= 2;
+  const float cc = odd ? sp : cp, ss = odd ? cp : sp;
+  c = neg_c ? -cc : cc;
+  s = neg_s ? -ss : ss;
+}
+// Math.hpp:26-43 RandUnitVec3 (uniform on the unit sphere) by the inverse-CDF map z = 1 - 2u,
+// phi = 2 pi v: two uniforms and no rejection loop, so a wave never waits on its unluckiest
+// lane's retries (the oracle draws the same map; DESIGN.md "Sampling").
 __device__ __forceinline__ f3 rand_unit_vec3(Path& g) {
-  f3 p;
-  while (true) {
-    float u[3];
-    g.take<3>(u);
-    p = mk(rand_range(u[0], -1.0f, 1.0f), rand_range(u[1], -1.0f, 1.0f), rand_range(u[2], -1.0f, 1.0f));
-    float lsq = dot(p, p);
-    if (lsq > 0.0f && lsq <= 1.0f) break;  // 1e-160 < |p|^2 <= 1 for a float |p|^2
-  }
-  return normalize(p);
+  float u[2];
+  g.take<2>(u);
+  const float z = 1.0f - 2.0f * u[0];
+  const float r = sqrtf(1.0f - z * z);
+  float c, s;
+  cos_sin_2pi(u[1], c, s);
+  return mk(r * c, r * s, z);
 }
 // NearZero: |x| < 1e-8 (double) <=> |x| <= 1e-8f for floats
 __device__ __forceinline__ bool near_zero(f3 v) {
@@ -994,14 +1013,13 @@ __device__ __forceinline__ void camera_ray(const RenderParams& P, int s_i, int s
   f3 c = mk(C.center[0], C.center[1], C.center[2]);
   if constexpr (Has<F, kFeatDefocus>()) {
     if (defocus) {
-      float dx, dy;
-      while (true) {  // RandInUnitDisk (x drawn before y)
-        float w[2];
-        g.take<2>(w);
-        dx = rand_range(w[0], -1.0f, 1.0f);
-        dy = rand_range(w[1], -1.0f, 1.0f);
-        if ((dx * dx + dy * dy) + 0.0f * 0.0f < 1.0f) break;
-      }
+      // RandInUnitDisk (uniform in the unit disk) by the inverse-CDF map r = sqrt(u), phi = 2 pi v
+      float w[2];
+      g.take<2>(w);
+      const float rr = sqrtf(w[0]);
+      float cd, sd;
+      cos_sin_2pi(w[1], cd, sd);
+      const float dx = rr * cd, dy = rr * sd;
       c = (c + (dx * mk(C.defocus_u[0], C.defocus_u[1], C.defocus_u[2]))) +
           (dy * mk(C.defocus_v[0], C.defocus_v[1], C.defocus_v[2]));
       u[2] = g.uniform();
@@ -1128,6 +1146,18 @@ __global__ __launch_bounds__(kBlock, RT2_MIN_WAVES_PER_EU) void render_kernel(co
         if constexpr (kMode == kModeLinear) {
           resolve_hit<F>(Nodes<kModeLinear>{reinterpret_cast<const float4*>(P.lind)}, h, ro, rd, rtime, hp, hn, front,
                          mat);
+#if RT2_EXP_TWICE & 1
+          {
+            f3 ro2 = ro, hp2, hn2;
+            bool fr2;
+            uint32_t m2;
+            asm volatile("" : "+v"(ro2.x), "+v"(ro2.y), "+v"(ro2.z));
+            resolve_hit<F>(Nodes<kModeLinear>{reinterpret_cast<const float4*>(P.lind)}, h, ro2, rd, rtime, hp2, hn2,
+                           fr2, m2);
+            asm volatile("" ::"v"(hp2.x), "v"(hp2.y), "v"(hp2.z), "v"(hn2.x), "v"(hn2.y), "v"(hn2.z), "v"(m2),
+                         "v"((int)fr2));
+          }
+#endif
         } else {
           resolve_hit<F>(N, h, ro, rd, rtime, hp, hn, front, mat);
         }
@@ -1141,6 +1171,14 @@ __global__ __launch_bounds__(kBlock, RT2_MIN_WAVES_PER_EU) void render_kernel(co
           bool dielectric = Has<F, kFeatSpecular>() && type == kMatDielectric;
           f3 ru = mk(0.0f, 0.0f, 0.0f);
           if (!dielectric) ru = rand_unit_vec3(path);  // one sampling site for every other material
+#if RT2_EXP_TWICE & 2
+          {
+            Path p2 = path;
+            asm volatile("" : "+v"(p2.n), "+v"(p2.frame));
+            f3 r2 = rand_unit_vec3(p2);
+            asm volatile("" ::"v"(r2.x), "v"(r2.y), "v"(r2.z));
+          }
+#endif
           if (Has<F, kFeatSpecular>() && type == kMatMetal) {
             dir = normalize(reflect(rd, hn)) + (m1.x * ru);
             att = mk(m0.y, m0.z, m0.w);
@@ -1183,6 +1221,17 @@ __global__ __launch_bounds__(kBlock, RT2_MIN_WAVES_PER_EU) void render_kernel(co
       int f = (int)path.frame + 1;
       if (f < frame_end) {
         path.start((uint32_t)f);
+#if RT2_EXP_TWICE & 4
+        {
+          Path p2 = path;
+          f3 o2, d2;
+          float t2;
+          int f2 = f;
+          asm volatile("" : "+v"(p2.frame), "+v"(f2));
+          camera_ray<F>(P, f2 % sq, f2 / sq % sq, p2, o2, d2, t2);
+          asm volatile("" ::"v"(o2.x), "v"(d2.x), "v"(d2.y), "v"(d2.z), "v"(t2));
+        }
+#endif
         camera_ray<F>(P, f % sq, f / sq % sq, path, ro, rd, rtime);
         thr = mk(1, 1, 1);
         depth_left = P.max_depth;
