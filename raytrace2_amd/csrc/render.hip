@@ -51,7 +51,7 @@ constexpr int kBlock = 256;
 #define RT2_EXP_NO_FIN_AABB 0  // ablation: always the reference-order slab test
 #endif
 #ifndef RT2_EXP_NO_UNIT_QUAD
-#define RT2_EXP_NO_UNIT_QUAD 1  // unit-normal quads take the general axis-aligned test (measured faster: fewer SALU)
+#define RT2_EXP_NO_UNIT_QUAD 0  // ablation: unit-normal quads take the general axis-aligned test
 #endif
 #ifndef RT2_EXP_TRACE_TWICE
 #define RT2_EXP_TRACE_TWICE 0  // cost probe: every ray is traced a second time (result discarded)
@@ -746,7 +746,7 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
   bool fin = wfin;  // inv finite: the NaN-free slab test applies
   const float tmin = 0.001f;
   float tmax = FLT_MAX;
-  bool any = false;
+  uint32_t prim = kRefNone;  // closest primitive so far (h.xf: its transform, quads: from the record)
   uint32_t cur_xf = kRefNone;
   uint32_t next = 0;  // this lane's next step
   const uint32_t len = P.lin_len;
@@ -823,15 +823,11 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
         }
         if (ok0 && tmin <= t0 && t0 <= tmax) {
           tmax = t0;
-          any = true;
-          h.prim = make_ref(kQuad, o0);
-          h.xf = cur_xf;
+          prim = make_ref(kQuad, o0);
         }
         if (ok1 && tmin <= t1 && t1 <= tmax) {
           tmax = t1;
-          any = true;
-          h.prim = make_ref(kQuad, o0 + 5u);
-          h.xf = cur_xf;
+          prim = make_ref(kQuad, o0 + 5u);
         }
       }
       next = i + run;
@@ -840,8 +836,7 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
       uint32_t ref = make_ref(kind, off);
       if (prim_t<F>(N, ref, o, d, time, tmin, tmax, t, cnt)) {
         tmax = t;
-        any = true;
-        h.prim = ref;
+        prim = ref;
         h.xf = cur_xf;
       }
     } else if (Has<F, kFeatXform>() && kind == kXform) {
@@ -874,16 +869,24 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
       float t;
       if (medium_t<F>(N, off, o, d, time, tmin, tmax, path, t, cnt)) {
         tmax = t;
-        any = true;
-        h.prim = make_ref(kMedium, off);
+        prim = make_ref(kMedium, off);
         h.xf = cur_xf;
       }
     }
   }
   h.t = tmax;
-  return any;
+  h.prim = prim;
+  if constexpr (Has<F, kFeatXform>()) {
+    if (prim != kRefNone && (prim >> 28) == kQuad) h.xf = N.word((prim & kOffsetMask) + 3u, 3);
+  }
+  return prim != kRefNone;
 }
 
+// Threaded traversal (small scenes): all lanes of the wave walk the pre-order program P.lin in
+// lockstep. Each lane keeps the index of its next step; the wave executes the smallest pending
+// index, so the step kind is wave-uniform (no divergence between kinds) and the step's program
+// entry and record are scalar loads into SGPRs. A lane whose AABB test misses jumps to the node's
+// skip index. Per lane the visit order is exactly the stack traversal's.
 // The closest hit's record in world space (what the reference's rec holds after the chain of
 // TransformedHittable::Hit returns): point, normal, front_face, material.
 template <uint32_t F, int kMode>
