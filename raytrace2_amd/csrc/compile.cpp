@@ -18,6 +18,7 @@ struct Flattener {
   CompiledScene& out;
   std::unordered_map<int, uint32_t> ref_of;  // obj index -> node ref (DAG sharing)
   std::unordered_map<int, int> acc_depth;    // accelerated list obj -> tree depth
+  std::unordered_map<uint32_t, uint32_t> lind_axis;  // program quad record -> axis code
   bool accelerate_lists = true;
   std::unordered_map<int, bool> medium_memo;
 
@@ -340,7 +341,21 @@ struct Flattener {
       }
       case kQuad: {
         uint32_t off = CopyRecords(src, kQuadRecords, lind);
-        lind[4 * (off + 3) + 3] = Bits(parent_xf);  // enclosing transform of this occurrence
+        uint32_t axis;
+        memcpy(&axis, &lind[4 * (off + 2) + 3], 4);
+        lind_axis[off] = axis;
+        if (axis >= 4 && axis <= 6) {  // QUADAA layout (rt2_layout.h)
+          const int k = (int)axis - 4, a = (k + 1) % 3, b = (k + 2) % 3;
+          const float* r = out.nodes.data() + 4 * (size_t)src;
+          const float n[3] = {r[0], r[1], r[2]}, d = r[3], q[3] = {r[4], r[5], r[6]}, mat = r[7];
+          const float u[3] = {r[8], r[9], r[10]}, v[3] = {r[12], r[13], r[14]}, w[3] = {r[16], r[17], r[18]};
+          const float sd = r[19];
+          const float rec[20] = {sd,   w[k], q[a], q[b], u[a], u[b],        v[a], v[b], n[0], n[1],
+                                 n[2], d,    q[0], q[1], q[2], mat, Bits(axis), Bits(parent_xf), 0, 0};
+          std::copy(rec, rec + 20, lind.begin() + 4 * (long)off);
+        } else {
+          lind[4 * (off + 3) + 3] = Bits(parent_xf);  // enclosing transform of this occurrence
+        }
         emit(kQuad, off, 0);
         return lin.size() / 4 <= (size_t)kLinearMaxSteps;
       }
@@ -470,8 +485,16 @@ bool CompileScene(const Scene& s, CompiledScene& out, std::string& err, bool acc
     for (size_t i = n; i-- > 0;) {
       if (out.lin[4 * i] != kQuad) continue;
       uint32_t run = 1;
-      if (i + 1 < n && out.lin[4 * (i + 1)] == kQuad && !entry[i + 1]) run = out.lin[4 * (i + 1) + 3] + 1;
+      if (i + 1 < n && out.lin[4 * (i + 1)] == kQuad && !entry[i + 1])
+        run = std::min(out.lin[4 * (i + 1) + 3] + 1, kLinearMaxRun);
       out.lin[4 * i + 3] = run;
+    }
+    // axis codes of each run's quads, 3 bits each, in the skip word
+    for (size_t i = 0; i < n; i++) {
+      if (out.lin[4 * i] != kQuad) continue;
+      uint32_t codes = 0;
+      for (uint32_t k = 0; k < out.lin[4 * i + 3]; k++) codes |= fl.lind_axis.at(out.lin[4 * (i + k) + 2]) << (3 * k);
+      out.lin[4 * i + 1] = codes;
     }
   }
   PackMaterials(s, out);

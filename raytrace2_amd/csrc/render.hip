@@ -149,6 +149,12 @@ __device__ __forceinline__ u32x16 sld16(const void* base, uint32_t off) {
   asm("s_load_dwordx16 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(base), "s"(off));
   return v;
 }
+// two 8-dword loads
+__device__ __forceinline__ void sld8x2(const void* base, uint32_t off0, uint32_t off1, u32x8& a, u32x8& b) {
+  asm("s_load_dwordx8 %0, %2, %3\n\ts_load_dwordx8 %1, %2, %4\n\ts_waitcnt lgkmcnt(0)"
+      : "=&s"(a), "=&s"(b)
+      : "s"(base), "s"(off0), "s"(off1));
+}
 // 20 dwords (one quad record) at off
 __device__ __forceinline__ void sld20(const void* base, uint32_t off, u32x16& a, u32x4& b) {
   asm("s_load_dwordx16 %0, %2, %3\n\ts_load_dwordx4 %1, %2, %4\n\ts_waitcnt lgkmcnt(0)"
@@ -465,6 +471,26 @@ __device__ __forceinline__ bool quad_cand_unit(const float* w, f3 o, f3 d, f3 in
   t_out = t;
   return !(fabsf(dk) <= 1e-8f) && (0.0f <= alpha && alpha <= 1.0f) && (0.0f <= beta && beta <= 1.0f);
 }
+// Unit-normal axis-aligned Quad::Hit from a QUADAA record r = (sD, w[K], q[A], q[B], u[A], u[B],
+// v[A], v[B]): the same operations as quad_cand_unit on the same values.
+template <int K>
+__device__ __forceinline__ bool quad_aa(const float* r, f3 o, f3 d, f3 inv, float& t_out) {
+  constexpr int A = (K + 1) % 3, B = (K + 2) % 3;
+  const float dk = comp<K>(d);
+  const float t = div_by_inv(r[0] - comp<K>(o), dk, comp<K>(inv));
+  const float pva = (comp<A>(o) + comp<A>(d) * t) - r[2];
+  const float pvb = (comp<B>(o) + comp<B>(d) * t) - r[3];
+  const float alpha = r[1] * (pva * r[7] - r[6] * pvb);  // w . cross(pv, v)
+  const float beta = r[1] * (r[4] * pvb - pva * r[5]);   // w . cross(u, pv)
+  t_out = t;
+  return !(fabsf(dk) <= 1e-8f) && (0.0f <= alpha && alpha <= 1.0f) && (0.0f <= beta && beta <= 1.0f);
+}
+__device__ __forceinline__ bool quad_aa_k(uint32_t k, const float* r, f3 o, f3 d, f3 inv, float& t) {
+  if (k == 0u) return quad_aa<0>(r, o, d, inv, t);
+  if (k == 1u) return quad_aa<1>(r, o, d, inv, t);
+  return quad_aa<2>(r, o, d, inv, t);
+}
+
 // quad candidate dispatched on a wave-uniform axis code
 __device__ __forceinline__ bool quad_cand_u(uint32_t axis, const float* w, f3 o, f3 d, f3 inv, float& t) {
   switch (axis) {
@@ -787,47 +813,66 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
 #endif
       if (!in) next = st.y;
     } else if (kind == kQuad) {
-      // a run of st.w quads with contiguous records: two candidates in flight, applied in order
+      // a run of st.w quads with contiguous records, axis codes in st.y (3 bits each); two
+      // unit-normal axis-aligned quads (QUADAA records, 8 words each) are tested per trip
       const uint32_t run = st.w;
-      for (uint32_t k = 0; k < run; k += 2) {
+      uint32_t codes = st.y;
+      for (uint32_t k = 0; k < run;) {
         const uint32_t o0 = off + 5u * k;
-        float w0[20], w1[20];
-        float t0, t1;
-        bool ok0, ok1 = false;
-        if (k + 1 < run) {
-          u32x16 a, b2;
-          u32x8 c;
-          sld40(recs, o0 * 16u, a, b2, c);
+        const uint32_t c0 = codes & 7u, c1 = (codes >> 3) & 7u;
+        if (k + 1 < run && c0 >= 4u && c1 >= 4u) {
+          u32x8 a, b;
+          sld8x2(recs, o0 * 16u, (o0 + 5u) * 16u, a, b);
+          float ra[8], rb[8];
 #pragma unroll
-          for (int j = 0; j < 16; j++) w0[j] = uf(a[j]);
-#pragma unroll
-          for (int j = 0; j < 4; j++) w0[16 + j] = uf(b2[j]);
-#pragma unroll
-          for (int j = 0; j < 12; j++) w1[j] = uf(b2[4 + j]);
-#pragma unroll
-          for (int j = 0; j < 8; j++) w1[12 + j] = uf(c[j]);
-          ok0 = quad_cand_u(a[11], w0, o, d, inv, t0);
-          ok1 = quad_cand_u(b2[15], w1, o, d, inv, t1);
+          for (int j = 0; j < 8; j++) {
+            ra[j] = uf(a[j]);
+            rb[j] = uf(b[j]);
+          }
+          float t0, t1;
+          const bool ok0 = quad_aa_k(c0 - 4u, ra, o, d, inv, t0);
+          const bool ok1 = quad_aa_k(c1 - 4u, rb, o, d, inv, t1);
           if (kStats) cnt.quad += 2;
+          if (ok0 && tmin <= t0 && t0 <= tmax) {
+            tmax = t0;
+            prim = make_ref(kQuadAA, o0);
+          }
+          if (ok1 && tmin <= t1 && t1 <= tmax) {
+            tmax = t1;
+            prim = make_ref(kQuadAA, o0 + 5u);
+          }
+          k += 2;
+          codes >>= 6;
         } else {
-          u32x16 a;
-          u32x4 b2;
-          sld20(recs, o0 * 16u, a, b2);
+          float t0;
+          bool ok0;
+          uint32_t kind0;
+          if (c0 >= 4u) {
+            const u32x8 a = sld8(recs, o0 * 16u);
+            float ra[8];
 #pragma unroll
-          for (int j = 0; j < 16; j++) w0[j] = uf(a[j]);
+            for (int j = 0; j < 8; j++) ra[j] = uf(a[j]);
+            ok0 = quad_aa_k(c0 - 4u, ra, o, d, inv, t0);
+            kind0 = kQuadAA;
+          } else {
+            u32x16 a;
+            u32x4 b2;
+            sld20(recs, o0 * 16u, a, b2);
+            float w0[20];
 #pragma unroll
-          for (int j = 0; j < 4; j++) w0[16 + j] = uf(b2[j]);
-          ok0 = quad_cand_u(a[11], w0, o, d, inv, t0);
-          t1 = 0.0f;
+            for (int j = 0; j < 16; j++) w0[j] = uf(a[j]);
+#pragma unroll
+            for (int j = 0; j < 4; j++) w0[16 + j] = uf(b2[j]);
+            ok0 = quad_cand_u(c0, w0, o, d, inv, t0);
+            kind0 = kQuad;
+          }
           if (kStats) cnt.quad += 1;
-        }
-        if (ok0 && tmin <= t0 && t0 <= tmax) {
-          tmax = t0;
-          prim = make_ref(kQuad, o0);
-        }
-        if (ok1 && tmin <= t1 && t1 <= tmax) {
-          tmax = t1;
-          prim = make_ref(kQuad, o0 + 5u);
+          if (ok0 && tmin <= t0 && t0 <= tmax) {
+            tmax = t0;
+            prim = make_ref(kind0, o0);
+          }
+          k += 1;
+          codes >>= 3;
         }
       }
       next = i + run;
@@ -878,6 +923,7 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
   h.prim = prim;
   if constexpr (Has<F, kFeatXform>()) {
     if (prim != kRefNone && (prim >> 28) == kQuad) h.xf = N.word((prim & kOffsetMask) + 3u, 3);
+    if (prim != kRefNone && (prim >> 28) == kQuadAA) h.xf = N.word((prim & kOffsetMask) + 4u, 1);
   }
   return prim != kRefNone;
 }
@@ -907,6 +953,11 @@ __device__ __forceinline__ void resolve_hit(const Nodes<kMode>& N, const HitRef&
     front = dot(d, outward) < 0.0f;
     n = front ? outward : -outward;
     mat = bits(r1.w);
+  } else if (kMode == kModeLinear && kind == kQuadAA) {
+    f3 qn = xyz(N[off + 2]);
+    front = dot(d, qn) < 0.0f;
+    n = front ? qn : -qn;
+    mat = N.word(off + 3, 3);
   } else {
     f3 qn = xyz(N[off]);
     front = dot(d, qn) < 0.0f;

@@ -27,6 +27,7 @@ enum NodeKind : uint32_t {
   kListAcc = 7,    // a large leaf-only sphere list with its exact acceleration tree
   kAccBvh = 8,     // 8 + split axis (8, 9, 10): node of a list's acceleration tree
   kAccSphere = 11, // a sphere reached through a list's acceleration tree
+  kQuadAA = 12,    // threaded program only: a unit-normal axis-aligned quad in the QUADAA layout
 };
 inline constexpr bool is_acc_bvh(uint32_t kind) { return kind - kAccBvh < 3u; }
 constexpr int kListAccelMin = 32;  // leaf-only sphere lists at least this long get a tree
@@ -42,6 +43,10 @@ inline constexpr uint32_t make_ref(uint32_t kind, uint32_t off) { return (kind <
 //          axis = k + 1 when n and w are exactly zero off axis k (exact axis-aligned test),
 //          k + 4 when moreover n[k] = s = +-1 exactly (sD = s * D), else 0
 //          In the threaded program's record copy (lind), v.w = the enclosing XFORM's lind ref.
+//  QUADAA: (threaded-program record copy of a quad with axis code K + 4)
+//          (sD, w[K], q[A], q[B]) (u[A], u[B], v[A], v[B]) (n.xyz, D) (q.xyz, material bits)
+//          (axis bits, xform ref bits, 0, 0), A = (K + 1) % 3, B = (K + 2) % 3: the test reads
+//          the first 8 words only
 //  SPHERE: (c0.xyz, radius) (displacement.xyz, material bits)
 //  LIST  : (count bits, flags bits, 0, 0) then child refs, 4 per record. flags bit0 = every
 //          child is a QUAD or SPHERE (iterated inline, no stack traffic).
@@ -99,8 +104,9 @@ constexpr int kLdsSceneBytesMax = 96 * 1024;  // scenes up to this size are stag
 // scene tree, one 16-byte entry per step: (kind, skip, record offset, aux).
 //   kind kBvh: skip = index after the node's subtree (taken when the AABB test misses)
 //   kind kQuad / kSphere / kMedium: record of the primitive; the next step is always index + 1;
-//     for kQuad, aux = length of the run of consecutive quads starting here with no skip target
-//     inside it (tested as a batch: the candidate math of two quads is interleaved)
+//     for kQuad, aux = length of the run of consecutive quads starting here (at most
+//     kLinearMaxRun) with no skip target inside it, skip = the run's axis codes, 3 bits per quad
+//     (codes 4..6 use the QUADAA record layout, the others the QUAD layout)
 //   kind kXform: enter the transform (record = XFORM record, skip = index of its kXformExit);
 //     the kernel walks the steps up to the exit in a nested loop with the transformed ray
 //   kind kXformExit: leave it (record = XFORM record, aux = parent XFORM ref or kRefNone)
@@ -110,6 +116,7 @@ constexpr int kLdsSceneBytesMax = 96 * 1024;  // scenes up to this size are stag
 // All lanes of a wave walk this array in lockstep at the smallest pending index, so the step
 // kind is wave-uniform and its record is read with scalar loads.
 constexpr int kLinearMaxSteps = 1024;  // scenes whose program is longer use the stack traversal
+constexpr uint32_t kLinearMaxRun = 10;  // quads per run (3-bit axis codes in one word)
 constexpr int kLinearMaxXformDepth = 8;  // deeper transform nesting uses the stack traversal
 
 enum TraversalMode : int { kModeStackGlobal = 0, kModeStackLds = 1, kModeLinear = 2 };
