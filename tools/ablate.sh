@@ -7,7 +7,7 @@ VARIANTS="${VARIANTS_LIST:-base: noballot:-DRT2_EXP_NO_BALLOT=1 cheaprng:-DRT2_E
 if [ "$MODE" = build ]; then
   mkdir -p $R/raytrace2_amd/lib/ablate
   for v in $VARIANTS; do
-    name=${v%%:*}; flags=${v#*:}
+    name=${v%%:*}; flags=$(echo "${v#*:}" | tr "," " ")
     make -s -C $R/raytrace2_amd/csrc clean >/dev/null
     make -s -j8 -C $R/raytrace2_amd/csrc HIPFLAGS_EXTRA="$flags" >/dev/null || exit 1
     cp $R/raytrace2_amd/lib/librt2.so $R/raytrace2_amd/lib/ablate/$name.so
