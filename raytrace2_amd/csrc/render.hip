@@ -149,24 +149,11 @@ __device__ __forceinline__ u32x16 sld16(const void* base, uint32_t off) {
   asm("s_load_dwordx16 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(base), "s"(off));
   return v;
 }
-// two 8-dword loads
-__device__ __forceinline__ void sld8x2(const void* base, uint32_t off0, uint32_t off1, u32x8& a, u32x8& b) {
-  asm("s_load_dwordx8 %0, %2, %3\n\ts_load_dwordx8 %1, %2, %4\n\ts_waitcnt lgkmcnt(0)"
-      : "=&s"(a), "=&s"(b)
-      : "s"(base), "s"(off0), "s"(off1));
-}
 // 20 dwords (one quad record) at off
 __device__ __forceinline__ void sld20(const void* base, uint32_t off, u32x16& a, u32x4& b) {
   asm("s_load_dwordx16 %0, %2, %3\n\ts_load_dwordx4 %1, %2, %4\n\ts_waitcnt lgkmcnt(0)"
       : "=&s"(a), "=&s"(b)
       : "s"(base), "s"(off), "s"(off + 64u));
-}
-// 40 dwords (two consecutive quad records) at off
-__device__ __forceinline__ void sld40(const void* base, uint32_t off, u32x16& a, u32x16& b, u32x8& c) {
-  asm("s_load_dwordx16 %0, %3, %4\n\ts_load_dwordx16 %1, %3, %5\n\ts_load_dwordx8 %2, %3, %6\n\t"
-      "s_waitcnt lgkmcnt(0)"
-      : "=&s"(a), "=&s"(b), "=&s"(c)
-      : "s"(base), "s"(off), "s"(off + 64u), "s"(off + 128u));
 }
 __device__ __forceinline__ float uf(uint32_t u) { return __uint_as_float(u); }
 
@@ -813,66 +800,39 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
 #endif
       if (!in) next = st.y;
     } else if (kind == kQuad) {
-      // a run of st.w quads with contiguous records, axis codes in st.y (3 bits each); two
-      // unit-normal axis-aligned quads (QUADAA records, 8 words each) are tested per trip
+      // a run of st.w quads with contiguous records, axis codes in st.y (3 bits each), tested in
+      // order (issue-bound: one candidate at a time beats two interleaved, measured)
       const uint32_t run = st.w;
       uint32_t codes = st.y;
-      for (uint32_t k = 0; k < run;) {
+      for (uint32_t k = 0; k < run; k++, codes >>= 3) {
         const uint32_t o0 = off + 5u * k;
-        const uint32_t c0 = codes & 7u, c1 = (codes >> 3) & 7u;
-        if (k + 1 < run && c0 >= 4u && c1 >= 4u) {
-          u32x8 a, b;
-          sld8x2(recs, o0 * 16u, (o0 + 5u) * 16u, a, b);
-          float ra[8], rb[8];
+        const uint32_t c0 = codes & 7u;
+        float t0;
+        bool ok0;
+        uint32_t kind0;
+        if (c0 >= 4u) {
+          const u32x8 a = sld8(recs, o0 * 16u);
+          float ra[8];
 #pragma unroll
-          for (int j = 0; j < 8; j++) {
-            ra[j] = uf(a[j]);
-            rb[j] = uf(b[j]);
-          }
-          float t0, t1;
-          const bool ok0 = quad_aa_k(c0 - 4u, ra, o, d, inv, t0);
-          const bool ok1 = quad_aa_k(c1 - 4u, rb, o, d, inv, t1);
-          if (kStats) cnt.quad += 2;
-          if (ok0 && tmin <= t0 && t0 <= tmax) {
-            tmax = t0;
-            prim = make_ref(kQuadAA, o0);
-          }
-          if (ok1 && tmin <= t1 && t1 <= tmax) {
-            tmax = t1;
-            prim = make_ref(kQuadAA, o0 + 5u);
-          }
-          k += 2;
-          codes >>= 6;
+          for (int j = 0; j < 8; j++) ra[j] = uf(a[j]);
+          ok0 = quad_aa_k(c0 - 4u, ra, o, d, inv, t0);
+          kind0 = kQuadAA;
         } else {
-          float t0;
-          bool ok0;
-          uint32_t kind0;
-          if (c0 >= 4u) {
-            const u32x8 a = sld8(recs, o0 * 16u);
-            float ra[8];
+          u32x16 a;
+          u32x4 b2;
+          sld20(recs, o0 * 16u, a, b2);
+          float w0[20];
 #pragma unroll
-            for (int j = 0; j < 8; j++) ra[j] = uf(a[j]);
-            ok0 = quad_aa_k(c0 - 4u, ra, o, d, inv, t0);
-            kind0 = kQuadAA;
-          } else {
-            u32x16 a;
-            u32x4 b2;
-            sld20(recs, o0 * 16u, a, b2);
-            float w0[20];
+          for (int j = 0; j < 16; j++) w0[j] = uf(a[j]);
 #pragma unroll
-            for (int j = 0; j < 16; j++) w0[j] = uf(a[j]);
-#pragma unroll
-            for (int j = 0; j < 4; j++) w0[16 + j] = uf(b2[j]);
-            ok0 = quad_cand_u(c0, w0, o, d, inv, t0);
-            kind0 = kQuad;
-          }
-          if (kStats) cnt.quad += 1;
-          if (ok0 && tmin <= t0 && t0 <= tmax) {
-            tmax = t0;
-            prim = make_ref(kind0, o0);
-          }
-          k += 1;
-          codes >>= 3;
+          for (int j = 0; j < 4; j++) w0[16 + j] = uf(b2[j]);
+          ok0 = quad_cand_u(c0, w0, o, d, inv, t0);
+          kind0 = kQuad;
+        }
+        if (kStats) cnt.quad += 1;
+        if (ok0 && tmin <= t0 && t0 <= tmax) {
+          tmax = t0;
+          prim = make_ref(kind0, o0);
         }
       }
       next = i + run;
