@@ -57,6 +57,7 @@ def lib():
         L.oracle_scene_hit.argtypes = [vp, fp, fp, ctypes.c_float, ctypes.c_float, ctypes.c_float, u64, fp]
         L.oracle_philox.argtypes = [ctypes.POINTER(ctypes.c_uint32)] * 3
         L.oracle_uniforms.argtypes = [u64, ctypes.c_uint32, ctypes.c_uint32, i32, fp]
+        L.oracle_samples.argtypes = [i32, u64, ctypes.c_uint32, ctypes.c_uint32, i32, fp, fp]
         L.oracle_quad_hit.argtypes = [fp, fp]
         L.oracle_sphere_hit.argtypes = [fp, fp]
         L.oracle_aabb_hit.argtypes = [fp]
@@ -153,6 +154,26 @@ def philox(ctr, key):
 def uniforms(seed, pixel, frame, n):
     out = np.zeros(n, np.float32)
     lib().oracle_uniforms(seed, pixel, frame, n, _f(out))
+    return out
+
+
+def unit_vectors(seed, pixel, frame, n):
+    """n RandUnitVec3 draws (inverse-CDF map) from the path stream."""
+    out = np.zeros((n, 3), np.float32)
+    lib().oracle_samples(0, seed, pixel, frame, n, _f(np.zeros(1, np.float32)), _f(out))
+    return out
+
+
+def unit_disk(seed, pixel, frame, n):
+    out = np.zeros((n, 3), np.float32)
+    lib().oracle_samples(1, seed, pixel, frame, n, _f(np.zeros(1, np.float32)), _f(out))
+    return out
+
+
+def cos_sin_2pi(v):
+    v = np.ascontiguousarray(v, np.float32)
+    out = np.zeros((v.size, 2), np.float32)
+    lib().oracle_samples(2, 0, 0, 0, v.size, _f(v), _f(out))
     return out
 
 

@@ -1400,6 +1400,22 @@ void oracle_uniforms(uint64_t seed, uint32_t pixel, uint32_t frame, int n, float
   for (int i = 0; i < n; i++) out[i] = g.RandReal();
 }
 
+// n draws of RandUnitVec3 (which = 0) or RandInUnitDisk (which = 1) from the path stream of
+// (seed, pixel, frame), 3 floats each; which = 2: CosSin2Pi of the n uniforms in `in` (2 floats each)
+void oracle_samples(int which, uint64_t seed, uint32_t pixel, uint32_t frame, int n, const float* in, float* out) {
+  Rng g(seed, pixel, frame, kTagPath);
+  for (int i = 0; i < n; i++) {
+    if (which == 2) {
+      CosSin2Pi(in[i], out[2 * i], out[2 * i + 1]);
+      continue;
+    }
+    vec3 v = which == 0 ? RandUnitVec3(g) : RandInUnitDisk(g);
+    out[3 * i] = v.x;
+    out[3 * i + 1] = v.y;
+    out[3 * i + 2] = v.z;
+  }
+}
+
 // Build a quad and intersect: in = q(3) u(3) v(3) o(3) d(3) tmin tmax ; out = hit t p(3) n(3) front alpha beta
 int oracle_quad_hit(const float* in, float* out) {
   Quad q({in[0], in[1], in[2]}, {in[3], in[4], in[5]}, {in[6], in[7], in[8]}, 0);

@@ -121,15 +121,41 @@ def test_scene_hit_cornell_walls():
     assert h[0] == 1 and h[1] == pytest.approx(553.0) and h[9] == 3
 
 
-def test_rand_unit_vec3_moments():
-    # RandUnitVec3 (Math.hpp:26-43) = normalize of a rejection sample in the unit ball, fed by the
-    # path stream: acceptance rate pi/6 and isotropic moments.
-    u = O.uniforms(99, 1, 2, 3 * 20000).reshape(-1, 3) * 2 - 1
+def test_rand_unit_vec3_distribution():
+    # RandUnitVec3 (Math.hpp:26-43) is uniform on the unit sphere; the restatement draws it by the
+    # inverse-CDF map (z = 1 - 2u, phi = 2 pi v): unit length, z uniform on [-1, 1] (Archimedes),
+    # isotropic first and second moments, and the same z / azimuth law as normalize(rejection
+    # sample in the unit ball) drawn from the same stream.
+    v = O.unit_vectors(99, 1, 2, 40000).astype(np.float64)
+    assert np.abs(np.linalg.norm(v, axis=1) - 1).max() < 1e-6
+    assert np.abs(v.mean(0)).max() < 0.02
+    assert (v * v).mean(0) == pytest.approx([1 / 3] * 3, abs=0.01)
+    z = np.sort(v[:, 2])
+    assert np.abs(z - np.linspace(-1, 1, z.size)).max() < 0.02  # uniform z
+    u = O.uniforms(7, 3, 4, 3 * 40000).reshape(-1, 3).astype(np.float64) * 2 - 1
     ok = ((u * u).sum(1) <= 1) & ((u * u).sum(1) > 0)
-    v = u[ok] / np.linalg.norm(u[ok], axis=1, keepdims=True)
-    assert ok.mean() == pytest.approx(math.pi / 6, abs=0.02)  # acceptance = ball / cube volume
-    assert np.abs(v.mean(0)).max() < 0.03
-    assert (v * v).mean(0) == pytest.approx([1 / 3] * 3, abs=0.02)
+    assert ok.mean() == pytest.approx(math.pi / 6, abs=0.01)  # the reference's acceptance rate
+    r = u[ok] / np.linalg.norm(u[ok], axis=1, keepdims=True)
+    for a in (v, r):
+        assert np.histogram(a[:, 2], bins=8, range=(-1, 1))[0].min() > a.shape[0] / 8 * 0.9
+
+
+def test_rand_in_unit_disk_distribution():
+    p = O.unit_disk(5, 6, 7, 40000).astype(np.float64)
+    r2 = (p[:, :2] ** 2).sum(1)
+    assert (p[:, 2] == 0).all() and r2.max() <= 1.0
+    assert np.abs(np.sort(r2) - np.linspace(0, 1, r2.size)).max() < 0.02  # r^2 uniform
+    assert np.abs(p[:, :2].mean(0)).max() < 0.02
+
+
+def test_cos_sin_2pi_polynomial():
+    # the shared quarter-turn polynomial (oracle CosSin2Pi == kernel cos_sin_2pi): max error 3e-7
+    v = (np.arange(1 << 20, dtype=np.float64) / (1 << 20)).astype(np.float32)
+    cs = O.cos_sin_2pi(v).astype(np.float64)
+    ang = 2 * np.pi * v.astype(np.float64)
+    assert np.abs(cs[:, 0] - np.cos(ang)).max() < 3e-7
+    assert np.abs(cs[:, 1] - np.sin(ang)).max() < 3e-7
+    assert cs[0, 0] == 1.0 and cs[0, 1] == 0.0
 
 
 def test_medium_free_flight_fraction(tmp_path):
