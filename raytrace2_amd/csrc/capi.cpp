@@ -480,6 +480,7 @@ int rt2_tracer_set_launch_frames(rt2_tracer* t, int n) {
 
 int rt2_tracer_on_resize(rt2_tracer* t, int w, int h) {
   if (!t || w <= 0 || h <= 0) return Fail(RT2_ERR_INVALID, "dims must be positive");
+  if (w > 65535 || h > 65535) return Fail(RT2_ERR_INVALID, "dims must be at most 65535");
   int rc = Sync(t);
   if (rc != RT2_OK) return rc;
   t->width = w;
@@ -670,7 +671,7 @@ int rt2_tracer_get_stats(rt2_tracer* t, rt2_stats* o) {
 
 int rt2_selftest(int device, int which, uint64_t n, uint64_t seed, uint64_t* mismatches, uint64_t* checked) {
   if (!mismatches || !checked) return Fail(RT2_ERR_INVALID, "null argument");
-  if (which < 0 || which > 1) return Fail(RT2_ERR_INVALID, "unknown self-test");
+  if (which < 0 || which > 2) return Fail(RT2_ERR_INVALID, "unknown self-test");
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return Fail(RT2_ERR_HIP, "no HIP device available");
   HIP_TRY(hipSetDevice(device));

@@ -89,7 +89,36 @@ __device__ __forceinline__ float dot(f3 a, f3 b) {
 __device__ __forceinline__ f3 cross(f3 a, f3 b) {
   return mk(a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y);
 }
-__device__ __forceinline__ f3 normalize(f3 v) { return v * (1.0f / sqrtf(dot(v, v))); }
+// IEEE-exact 1/x and sqrt(x) without the range-scaling steps of the full sequences: equal to them
+// (v_div_scale / v_div_fixup and the sqrt rescale are identities there) for 2^-95 <= |x| <= 2^126
+// (reciprocal) and 2^-96 <= x <= 2^126 (sqrt); callers check the range wave-uniformly and take
+// the full sequence otherwise. rt2_selftest which 2 checks both on the GPU.
+__device__ __forceinline__ float rcp_nr(float x) {
+  const float r0 = __builtin_amdgcn_rcpf(x);
+  const float r1 = fmaf(fmaf(-x, r0, 1.0f), r0, r0);
+  const float q1 = fmaf(fmaf(-x, r1, 1.0f), r1, r1);
+  return fmaf(fmaf(-x, q1, 1.0f), r1, q1);
+}
+__device__ __forceinline__ float sqrt_nr(float x) {
+  const float s = __builtin_amdgcn_sqrtf(x);
+  const float sdn = __uint_as_float(__float_as_uint(s) - 1u), sup = __uint_as_float(__float_as_uint(s) + 1u);
+  const float rdn = fmaf(-sdn, s, x), rup = fmaf(-sup, s, x);
+  const float r = rdn <= 0.0f ? sdn : s;
+  return rup > 0.0f ? sup : r;
+}
+__device__ __forceinline__ bool rcp_in_range(float x) { return fabsf(x) >= 0x1p-95f && fabsf(x) <= 0x1p126f; }
+// glm::normalize = v * inversesqrt(dot(v, v)) = v * (1 / sqrt(dot(v, v)))
+__device__ __forceinline__ f3 normalize(f3 v) {
+  const float l2 = dot(v, v);
+  if (__all(l2 >= 0x1p-96f && l2 <= 0x1p126f)) return v * rcp_nr(sqrt_nr(l2));
+  return v * (1.0f / sqrtf(l2));
+}
+// (1/d.x, 1/d.y, 1/d.z), IEEE
+__device__ __forceinline__ f3 recip3(f3 d) {
+  if (__all(rcp_in_range(d.x) && rcp_in_range(d.y) && rcp_in_range(d.z)))
+    return mk(rcp_nr(d.x), rcp_nr(d.y), rcp_nr(d.z));
+  return mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+}
 __device__ __forceinline__ f3 xyz(float4 v) { return mk(v.x, v.y, v.z); }
 __device__ __forceinline__ uint32_t bits(float f) { return __float_as_uint(f); }
 // glm scalar max/min
@@ -199,6 +228,8 @@ __device__ __forceinline__ float to_unit(uint32_t v) { return (float)(v >> 8) * 
 // The per-lane path context the samplers need.
 struct Path {
   uint32_t k0, k1, pix, frame;
+  uint32_t xy;   // pixel x | y << 16 (global image coordinates)
+  uint32_t sij;  // stratum s_i | s_j << 16 of `frame` (RayTracer.cpp:59-60), advanced per frame
   uint32_t n;
   uint32_t r0, r1, r2, r3;
   __device__ __forceinline__ void start(uint32_t f) {
@@ -600,7 +631,7 @@ template <uint32_t F, int kMode, bool kStats>
 __device__ __forceinline__ bool trace_stack(const RenderParams& P, const Nodes<kMode>& N, f3 wo, f3 wd, float time,
                                             Path& path, HitRef& h, uint32_t* stk, Counters& cnt, bool& overflow) {
   f3 o = wo, d = wd;
-  const f3 winv = mk(1.0f / wd.x, 1.0f / wd.y, 1.0f / wd.z);
+  const f3 winv = recip3(wd);
   f3 inv = winv;
   const float tmin = 0.001f;  // Interval{0.001, kInfinity}
   float tmax = FLT_MAX;
@@ -656,7 +687,7 @@ __device__ __forceinline__ bool trace_stack(const RenderParams& P, const Nodes<k
         overflow = true;
       } else {
         to_model(N, off, o, d);
-        inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+        inv = recip3(d);
         cur_xf = cur;
         stk[(sp++) * kBlock] = make_ref(kXformExit, off);
         cur = N.word(off, 3);  // the transformed child is the next step
@@ -670,7 +701,7 @@ __device__ __forceinline__ bool trace_stack(const RenderParams& P, const Nodes<k
         inv = winv;
       } else {
         ray_in_space(N, cur_xf, wo, wd, o, d);
-        inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+        inv = recip3(d);
       }
     } else if (Has<F, kFeatMedium>() && kind == kMedium) {
       if (kStats) cnt.medium++;
@@ -753,7 +784,7 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
   const void* prog = P.lin;
   const void* recs = P.lind;
   f3 o = wo, d = wd;
-  const f3 winv = mk(1.0f / wd.x, 1.0f / wd.y, 1.0f / wd.z);
+  const f3 winv = recip3(wd);
   f3 inv = winv;
   const bool wfin = finite3(winv);
   bool fin = wfin;  // inv finite: the NaN-free slab test applies
@@ -854,7 +885,7 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
                  uf(m[2]) * d.x + uf(m[6]) * d.y + uf(m[10]) * d.z);
       o = no;
       d = normalize(nd);
-      inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+      inv = recip3(d);
       fin = finite3(inv);
       cur_xf = make_ref(kXform, off);
     } else if (Has<F, kFeatXform>() && kind == kXformExit) {
@@ -866,7 +897,7 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
         fin = wfin;
       } else {
         ray_in_space(N, cur_xf, wo, wd, o, d);
-        inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+        inv = recip3(d);
         fin = finite3(inv);
       }
     } else if (Has<F, kFeatMedium>() && kind == kMedium) {
@@ -1007,10 +1038,10 @@ __device__ __forceinline__ f3 tex_value(const RenderParams& P, uint32_t idx, f3 
 
 // ------------------------------------------------------------------------------------------
 template <uint32_t F>
-__device__ __forceinline__ void camera_ray(const RenderParams& P, int s_i, int s_j, Path& g, f3& o, f3& d,
-                                           float& time) {
+__device__ __forceinline__ void camera_ray(const RenderParams& P, Path& g, f3& o, f3& d, float& time) {
   const CameraParams& C = P.cam;
-  int x = (int)(g.pix % (uint32_t)P.width), y = (int)(g.pix / (uint32_t)P.width);
+  const int x = (int)(g.xy & 0xFFFFu), y = (int)(g.xy >> 16);
+  const int s_i = (int)(g.sij & 0xFFFFu), s_j = (int)(g.sij >> 16);
   float u[3];
   bool defocus = Has<F, kFeatDefocus>() && !(C.defocus_angle <= 0.0f);
   if (defocus) {
@@ -1067,6 +1098,8 @@ __global__ __launch_bounds__(kBlock, RT2_MIN_WAVES_PER_EU) void render_kernel(co
   path.k0 = P.seed_lo;
   path.k1 = P.seed_hi;
   path.pix = 0;
+  path.xy = 0;
+  path.sij = 0;
   path.start(0);
   path.r0 = path.r1 = path.r2 = path.r3 = 0;
   f3 ro = mk(0, 0, 0), rd = mk(0, 0, 1), thr = mk(1, 1, 1);
@@ -1111,13 +1144,15 @@ __global__ __launch_bounds__(kBlock, RT2_MIN_WAVES_PER_EU) void render_kernel(co
         int y = ((r / P.band_h) * P.world + P.rank) * P.band_h + (r % P.band_h);
         lidx = (uint32_t)r * (uint32_t)P.width + (uint32_t)x;
         path.pix = (uint32_t)y * (uint32_t)P.width + (uint32_t)x;
+        path.xy = (uint32_t)x | ((uint32_t)y << 16);
         acc = mk(P.accum[3 * lidx], P.accum[3 * lidx + 1], P.accum[3 * lidx + 2]);
         item_rays = 0;
         if (P.frame_begin >= frame_end) continue;  // zero frames requested
         need = false;
         int f = P.frame_begin;
         path.start((uint32_t)f);
-        camera_ray<F>(P, f % sq, f / sq % sq, path, ro, rd, rtime);
+        path.sij = (uint32_t)(f % sq) | ((uint32_t)(f / sq % sq) << 16);
+        camera_ray<F>(P, path, ro, rd, rtime);
         thr = mk(1, 1, 1);
         depth_left = P.max_depth;
       }
@@ -1235,18 +1270,25 @@ __global__ __launch_bounds__(kBlock, RT2_MIN_WAVES_PER_EU) void render_kernel(co
       int f = (int)path.frame + 1;
       if (f < frame_end) {
         path.start((uint32_t)f);
+        {  // next stratum: (f % sq, f / sq % sq) from the previous frame's
+          uint32_t si = (path.sij & 0xFFFFu) + 1u, sj = path.sij >> 16;
+          if (si == (uint32_t)sq) {
+            si = 0u;
+            sj = sj + 1u == (uint32_t)sq ? 0u : sj + 1u;
+          }
+          path.sij = si | (sj << 16);
+        }
 #if RT2_EXP_TWICE & 4
         {
           Path p2 = path;
           f3 o2, d2;
           float t2;
-          int f2 = f;
-          asm volatile("" : "+v"(p2.frame), "+v"(f2));
-          camera_ray<F>(P, f2 % sq, f2 / sq % sq, p2, o2, d2, t2);
+          asm volatile("" : "+v"(p2.frame), "+v"(p2.sij));
+          camera_ray<F>(P, p2, o2, d2, t2);
           asm volatile("" ::"v"(o2.x), "v"(d2.x), "v"(d2.y), "v"(d2.z), "v"(t2));
         }
 #endif
-        camera_ray<F>(P, f % sq, f / sq % sq, path, ro, rd, rtime);
+        camera_ray<F>(P, path, ro, rd, rtime);
         thr = mk(1, 1, 1);
         depth_left = P.max_depth;
       } else {
@@ -1338,6 +1380,7 @@ KernelFn Kernel(int v, int mode, bool stats) {
 // Self-tests of the kernel's exact shortcuts on random inputs (rt2_selftest):
 //   which 0: div_by_inv(a, b, fl(1/b)) == a / b for |b| > 1e-8, |a / b| >= 1e-3 (accepted quad t)
 //   which 1: aabb_hit_fin == aabb_hit for rays with finite inv
+//   which 2: rcp_nr == 1/x and sqrt_nr == sqrt(x) in their ranges
 __device__ __forceinline__ float rand_float(uint32_t bits, int emin, int emax, uint32_t sel) {
   const int e = emin + (int)(sel % (uint32_t)(emax - emin + 1));
   return __uint_as_float((bits & 0x807FFFFFu) | ((uint32_t)(e + 127) << 23));
@@ -1356,6 +1399,13 @@ __global__ void selftest_kernel(int which, unsigned long long n, uint32_t seed, 
       checked++;
       const float inv = 1.0f / b;
       if (__float_as_uint(div_by_inv(a, b, inv)) != __float_as_uint(q)) bad++;
+    } else if (which == 2) {
+      // rcp_nr / sqrt_nr against IEEE 1/x and sqrt(x) over their whole ranges
+      const float x = rand_float(r0, -95, 125, r1);
+      const float y = fabsf(rand_float(r2, -96, 125, r3));
+      checked++;
+      if (__float_as_uint(rcp_nr(x)) != __float_as_uint(1.0f / x)) bad++;
+      if (__float_as_uint(sqrt_nr(y)) != __float_as_uint(sqrtf(y))) bad++;
     } else {
       uint32_t s0, s1, s2, s3;
       philox(seed, 0xAABBu, (uint32_t)idx, (uint32_t)(idx >> 32), 1u, s0, s1, s2, s3);
@@ -1364,7 +1414,7 @@ __global__ void selftest_kernel(int which, unsigned long long n, uint32_t seed, 
       const float lo_z = rand_float(s0, -4, 9, s1), hi_z = lo_z + rand_float(s1, -6, 8, s0 >> 7);
       const f3 o = mk(rand_float(s2, -3, 10, s3), rand_float(s3, -3, 10, s2 >> 5), rand_float(s2 ^ s3, -3, 10, s1));
       const f3 d = mk(rand_float(r0 ^ s0, -40, 1, r3), rand_float(r1 ^ s1, -40, 1, s3 >> 3), rand_float(r2 ^ s2, -40, 1, r0));
-      const f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+      const f3 inv = recip3(d);
       if (!finite3(inv)) continue;
       const float tmax = (s3 & 1u) ? FLT_MAX : rand_float(s0 ^ r3, -3, 12, s2);
       const float4 lo = make_float4(lo_x, lo_y, lo_z, 0.0f), hi = make_float4(hi_x, hi_y, hi_z, 0.0f);

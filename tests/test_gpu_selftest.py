@@ -5,13 +5,16 @@
   can accept the quotient (|b| > 1e-8, a / b >= tmin).
 * aabb_hit_fin: the NaN-free slab test must decide exactly like the reference's swap +
   glm::max/min chain with early exits (AABB.hpp:34-47) for every ray with a finite inverse.
+* rcp_nr / sqrt_nr: 1/x and sqrt(x) without the range-scaling steps equal the IEEE results over
+  the ranges where the kernel uses them (normalize, ray reciprocals).
 """
 import pytest
 
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("which,n", [(0, 1 << 28), (1, 1 << 26)], ids=["div_by_inv", "aabb_fin"])
+@pytest.mark.parametrize("which,n", [(0, 1 << 28), (1, 1 << 26), (2, 1 << 28)],
+                         ids=["div_by_inv", "aabb_fin", "rcp_sqrt_nr"])
 def test_selftest(have_gpu, which, n):
     from raytrace2_amd._native import selftest
     bad, checked = selftest(which, n, seed=20241015)
