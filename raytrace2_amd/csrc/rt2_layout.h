@@ -116,7 +116,10 @@ constexpr int kLdsSceneBytesMax = 96 * 1024;  // scenes up to this size are stag
 // All lanes of a wave walk this array in lockstep at the smallest pending index, so the step
 // kind is wave-uniform and its record is read with scalar loads.
 constexpr int kLinearMaxSteps = 1024;  // scenes whose program is longer use the stack traversal
-constexpr uint32_t kLinearMaxRun = 10;  // quads per run (3-bit axis codes in one word)
+#ifndef RT2_LINEAR_MAX_RUN
+#define RT2_LINEAR_MAX_RUN 10
+#endif
+constexpr uint32_t kLinearMaxRun = RT2_LINEAR_MAX_RUN;  // quads per run (3-bit axis codes in one word)
 constexpr int kLinearMaxXformDepth = 8;  // deeper transform nesting uses the stack traversal
 
 enum TraversalMode : int { kModeStackGlobal = 0, kModeStackLds = 1, kModeLinear = 2 };
