@@ -66,7 +66,7 @@ constexpr int kBlock = 256;
 #define RT2_EXP_STAMPS 0  // diagnostic build: per-section s_memtime sums into the stamp slots
 #endif
 #ifndef RT2_MIN_WAVES_PER_EU
-#define RT2_MIN_WAVES_PER_EU 1
+#define RT2_MIN_WAVES_PER_EU 0  // 0: per-variant occupancy targets (kMinWaves below)
 #endif
 
 extern __shared__ float4 s_dyn[];  // [lds_nodes scene records][stack_depth * kBlock stack words]
@@ -1075,8 +1075,21 @@ __device__ __forceinline__ void camera_ray(const RenderParams& P, Path& g, f3& o
   d = normalize(pc - c);
 }
 
+// Occupancy target (waves per SIMD the register allocation must allow) for the threaded-traversal
+// product kernels: the highest that compiles without VGPR spills. Stack-traversal and stats
+// kernels keep the compiler's own allocation (their LDS stack bounds occupancy anyway).
 template <uint32_t F, int kMode, bool kStats>
-__global__ __launch_bounds__(kBlock, RT2_MIN_WAVES_PER_EU) void render_kernel(const RenderParams P) {
+constexpr int MinWaves() {
+  if (RT2_MIN_WAVES_PER_EU > 0) return RT2_MIN_WAVES_PER_EU;
+  if (kStats || kMode != kModeLinear) return 1;
+  if (F == kFeatXform) return 6;                  // Cornell: 80 VGPRs
+  if (F == (kFeatXform | kFeatMedium)) return 5;  // Cornell volume: 95 VGPRs
+  if (F == kFeatAll) return 1;
+  return 6;                                       // book 1
+}
+
+template <uint32_t F, int kMode, bool kStats>
+__global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render_kernel(const RenderParams P) {
   Nodes<kMode> N{reinterpret_cast<const float4*>(P.nodes)};
   if constexpr (kMode == kModeStackLds) {
     const float4* src = reinterpret_cast<const float4*>(P.nodes);
