@@ -48,7 +48,13 @@ def parse():
     ap.add_argument("--seed", type=int, default=0x5EED2024)
     ap.add_argument("--band-h", type=int, default=16)
     ap.add_argument("--launch-frames", type=int, default=0, help="frames per kernel launch (0 = all)")
-    ap.add_argument("--cpu-frames", type=int, default=4, help="oracle sample: frames at full resolution")
+    ap.add_argument("--work-split", type=int, default=-1,
+                    help="work items (pixel x frame chunk) per resident lane (-1: library default, 0: no split)")
+    ap.add_argument("--batch-max", type=int, default=0, help="work items a wave reserves at once (0: default)")
+    ap.add_argument("--sample-budget-gb", type=float, default=0.0, help="per-frame sample buffer bound (0: default)")
+    ap.add_argument("--emulate-world", type=int, default=1,
+                    help="diagnostic: render only rank 0's row bands of an N-GPU split on this one GPU (no gather)")
+    ap.add_argument("--cpu-frames", type=int, default=48, help="oracle sample: frames at full resolution")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--stats-frames", type=int, default=8)
     ap.add_argument("--out-image", default="")
@@ -81,21 +87,29 @@ def main():
     tr.max_depth = a.max_depth
     tr.SetSamplesPerPixel(a.spp)
     tr.OnResize((a.width, a.height))
-    tr.set_partition(a.band_h, rank, world)
+    emulate = a.emulate_world if world == 1 and a.emulate_world > 1 else 1
+    tr.set_partition(a.band_h, rank, world * emulate)
     if a.launch_frames:
         tr.set_launch_frames(a.launch_frames)
+    if a.work_split >= 0:
+        tr.set_work_split(a.work_split)
+    if a.batch_max > 0:
+        tr.set_batch_max(a.batch_max)
+    if a.sample_budget_gb > 0:
+        tr.set_sample_budget(int(a.sample_budget_gb * (1 << 30)))
     tr.synchronize()
     setup_s = time.perf_counter() - t0
     rows = tr.local_rows()
     from raytrace2_amd.dist import BandGather
-    gath = BandGather(a.height, a.width, a.band_h, world, rank, dev)
-    assert gath.local_view().shape[0] == rows
+    gath = BandGather(a.height, a.width, a.band_h, world, rank, dev) if emulate == 1 else None
+    assert gath is None or gath.local_view().shape[0] == rows
 
     def step():
         tr.Reset()
         tr.Render(a.spp)
-        tr.copy_accum_to(gath.send.data_ptr(), stream.cuda_stream)
-        gath.gather()  # RCCL gather of the row bands to rank 0 + de-interleave
+        if gath is not None:
+            tr.copy_accum_to(gath.send.data_ptr(), stream.cuda_stream)
+            gath.gather()  # RCCL gather of the row bands to rank 0 + de-interleave
 
     for _ in range(a.warmup):
         step()
@@ -116,6 +130,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t_start
     st = tr.stats()
+    shape = tr.last_launch()
     stream_ms = ev0.elapsed_time(ev1)
     rays_local = st["rays"]
     kernel_ms = st["kernel_ms"]
@@ -130,7 +145,7 @@ def main():
     else:
         rays_total = float(rays_local)
 
-    if rank == 0 and a.out_image:
+    if rank == 0 and a.out_image and gath is not None:
         img = gath.image.cpu().numpy() / np.float32(a.spp)
         R.WriteImage(img, a.width, a.height, a.out_image)
 
@@ -149,7 +164,7 @@ def main():
         f_ray = sum(FLOPS.get(k, 0) * per_ray[k] for k in REC_BYTES)
         rays_per_launch = rays_local / launches
         pixels_local = rows * a.width
-        frame_bytes = pixels_local * (12 + 12 + 4)  # accum read + write, RGBA8 write per launch
+        frame_bytes = pixels_local * 12 * (a.spp * a.steps / launches)  # float3 sample store per frame
         bytes_per_launch = rays_per_launch * b_ray + frame_bytes
         avg_launch_s = kernel_ms / 1e3 / launches
         achieved = bytes_per_launch / avg_launch_s / 1e9
@@ -226,17 +241,21 @@ def main():
                     f"{a.seed:#x}",
             "config": {"workload": workload,
                        "parallelism": f"row-bands h={a.band_h} x {world} GPU(s), RCCL gather to rank 0",
-                       "launch_frames": a.launch_frames or a.spp},
+                       "launch_frames": a.spp * a.steps // launches,
+                       "work_split": shape},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "detail": {"rays": int(rays_total), "stream_ms": round(stream_ms, 2),
                        "kernel_ms_per_step": round(kernel_ms / a.steps, 2), "launches": launches,
                        "variant_features": hex(tr.last_variant_features()) if hasattr(tr, "last_variant_features") else None,
                        "setup_s": round(setup_s, 3), "stamps": st.get("stamps"),
-                       "rays_per_sample": round(rays_total / (a.steps * a.spp * a.width * a.height), 4)},
+                       "rays_per_sample": round(rays_total / (a.steps * a.spp * a.width * rows * world), 4)},
         }
         if cpu:
             out["detail"]["gpu_over_cpu"] = round(value / cpu["value"], 1)
+        if emulate > 1:
+            out["config"]["emulated"] = (f"rank 0 of {emulate}: {rows} of {a.height} rows on this GPU, no gather; "
+                                         "value is this GPU's rate, not a job rate")
         print(json.dumps(out), flush=True)
     tr.close()
     if world > 1:

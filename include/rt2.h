@@ -104,6 +104,18 @@ RT2_API int rt2_tracer_set_samples_per_pixel(rt2_tracer* tr, int spp); /* App.cp
 RT2_API int rt2_tracer_set_seed(rt2_tracer* tr, uint64_t seed);
 RT2_API int rt2_tracer_set_partition(rt2_tracer* tr, int band_h, int rank, int world);
 RT2_API int rt2_tracer_set_launch_frames(rt2_tracer* tr, int frames_per_launch); /* 0 = all */
+/* Work split: each pixel's frames of a launch are cut into chunks so that the launch holds about
+ * `items_per_lane` work items (pixel x frame chunk) per resident GPU lane (default 64; 0 = one chunk
+ * per pixel). Every frame's sample goes to a per-frame buffer and is summed in frame order after
+ * the launch, so results do not depend on the split. The buffer is bounded by `bytes` (default
+ * 16 GiB): a render needing more runs as several launches. */
+RT2_API int rt2_tracer_set_work_split(rt2_tracer* tr, int items_per_lane);
+RT2_API int rt2_tracer_set_sample_budget(rt2_tracer* tr, uint64_t bytes);
+/* Most work items a GPU wave reserves with one atomic (default 64); batches shrink as the launch
+ * drains. */
+RT2_API int rt2_tracer_set_batch_max(rt2_tracer* tr, int items);
+/* Launch shape of the last render: persistent workgroups, frames per work item, kernel variant. */
+RT2_API int rt2_tracer_last_launch(const rt2_tracer* tr, int* grid, int* chunk_frames, int* variant);
 RT2_API int rt2_tracer_on_resize(rt2_tracer* tr, int width, int height);
 RT2_API int rt2_tracer_reset(rt2_tracer* tr);
 RT2_API int rt2_tracer_update(rt2_tracer* tr);

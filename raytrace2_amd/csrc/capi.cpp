@@ -15,6 +15,8 @@
 namespace rt2 {
 hipError_t LaunchRender(const RenderParams& p, int variant, bool stats, int grid, hipStream_t stream);
 int RenderBlocksPerCU(int variant, int mode, bool stats, size_t lds_bytes);
+hipError_t LaunchAccumulate(const float* samples, float* accum, uint8_t* pixels, uint32_t npix, int n_frames,
+                            int frame_idx, hipStream_t stream);
 hipError_t LaunchSelftest(int which, unsigned long long n, uint32_t seed, unsigned long long* d_out, hipStream_t stream);
 int RenderMode(const RenderParams& p);
 int RenderBlockSize();
@@ -67,6 +69,14 @@ struct rt2_tracer {
   int max_depth = 50;
   uint64_t seed = 0x5EED2024ull;
   int launch_frames = 0;
+  // per-frame sample buffer ([frames][local pixels] float3) that lets a pixel's frames be split
+  // into chunks rendered by different lanes and still be summed in frame order
+  float* d_samples = nullptr;
+  size_t samples_bytes = 0;
+  size_t sample_budget = size_t(16) << 30;  // bytes; bounds the frames per launch
+  int work_split = 64;                     // target work items per resident lane (0: one chunk)
+  int batch_max = 64;                      // most work items a wave reserves with one atomic
+  int last_chunk_frames = 0;
   int last_variant = -1;
   int last_grid = 0;
   uint64_t launches = 0;
@@ -100,6 +110,9 @@ int LocalRows(int h, int band_h, int rank, int world) {
 }
 
 void FreeFrame(rt2_tracer* t) {
+  (void)hipFree(t->d_samples);
+  t->d_samples = nullptr;
+  t->samples_bytes = 0;
   (void)hipFree(t->d_accum);
   (void)hipFree(t->d_pixels);
   (void)hipFree(t->d_ray_counts);
@@ -478,6 +491,32 @@ int rt2_tracer_set_launch_frames(rt2_tracer* t, int n) {
   return RT2_OK;
 }
 
+int rt2_tracer_set_work_split(rt2_tracer* t, int items_per_lane) {
+  if (!t || items_per_lane < 0) return Fail(RT2_ERR_INVALID, "items_per_lane must be >= 0");
+  t->work_split = items_per_lane;
+  return RT2_OK;
+}
+
+int rt2_tracer_set_batch_max(rt2_tracer* t, int items) {
+  if (!t || items < 1) return Fail(RT2_ERR_INVALID, "batch must be >= 1");
+  t->batch_max = items;
+  return RT2_OK;
+}
+
+int rt2_tracer_set_sample_budget(rt2_tracer* t, uint64_t bytes) {
+  if (!t) return Fail(RT2_ERR_INVALID, "null tracer");
+  t->sample_budget = (size_t)bytes;
+  return RT2_OK;
+}
+
+int rt2_tracer_last_launch(const rt2_tracer* t, int* grid, int* chunk_frames, int* variant) {
+  if (!t) return Fail(RT2_ERR_INVALID, "null tracer");
+  if (grid) *grid = t->last_grid;
+  if (chunk_frames) *chunk_frames = t->last_chunk_frames;
+  if (variant) *variant = t->last_variant;
+  return RT2_OK;
+}
+
 int rt2_tracer_on_resize(rt2_tracer* t, int w, int h) {
   if (!t || w <= 0 || h <= 0) return Fail(RT2_ERR_INVALID, "dims must be positive");
   if (w > 65535 || h > 65535) return Fail(RT2_ERR_INVALID, "dims must be at most 65535");
@@ -522,12 +561,11 @@ int rt2_tracer_render(rt2_tracer* t, int n_frames) {
   p.rank = t->rank;
   p.world = t->world;
   p.tiles_x = (t->width + 7) / 8;
-  p.n_items = (uint32_t)p.tiles_x * (uint32_t)((t->local_rows + 7) / 8) * 64u;
+  p.tile_items = (uint32_t)p.tiles_x * (uint32_t)((t->local_rows + 7) / 8) * 64u;
+  p.local_pixels = (uint32_t)t->width * (uint32_t)t->local_rows;
   p.max_depth = t->max_depth;
   p.seed_lo = (uint32_t)t->seed;
   p.seed_hi = (uint32_t)(t->seed >> 32);
-  p.accum = t->d_accum;
-  p.pixels = t->d_pixels;
   p.ray_counts = t->d_ray_counts;
   p.work_counter = t->d_work;
   p.stats = t->d_stats;
@@ -539,21 +577,52 @@ int rt2_tracer_render(rt2_tracer* t, int n_frames) {
   p.lin_len = t->use_linear ? t->lin_len : 0u;
   uint32_t feats = t->features | (p.cam.defocus_angle > 0.0f ? (uint32_t)kFeatDefocus : 0u);
   int variant = RenderVariant(feats);
-  int grid = t->cus * RenderBlocksPerCU(variant, RenderMode(p), t->stats_on, RenderLdsBytes(p));
-  int64_t blocks_needed = ((int64_t)p.n_items + RenderBlockSize() - 1) / RenderBlockSize();
-  if (grid > blocks_needed) grid = (int)blocks_needed;
+  const int64_t resident = (int64_t)t->cus * RenderBlocksPerCU(variant, RenderMode(p), t->stats_on,
+                                                                 RenderLdsBytes(p)) * RenderBlockSize();
+  // frames per launch: the caller's launch_frames, bounded by the sample-buffer budget
+  const size_t frame_bytes = (size_t)p.local_pixels * 3 * sizeof(float);
+  int per_launch = t->launch_frames > 0 ? std::min(t->launch_frames, n_frames) : n_frames;
+  per_launch = (int)std::max<size_t>(1, std::min<size_t>((size_t)per_launch, t->sample_budget / frame_bytes));
+  const size_t need = (size_t)per_launch * frame_bytes;
+  if (need > t->samples_bytes) {
+    HIP_TRY(hipStreamSynchronize(t->stream));  // the old buffer may still be read
+    (void)hipFree(t->d_samples);
+    t->d_samples = nullptr;
+    t->samples_bytes = 0;
+    HIP_TRY(hipMalloc(&t->d_samples, need));
+    t->samples_bytes = need;
+  }
+  p.samples = t->d_samples;
   t->last_variant = variant;
-  t->last_grid = grid;
-  int chunk = t->launch_frames > 0 ? t->launch_frames : n_frames;
-  for (int done = 0; done < n_frames; done += chunk) {
+  for (int done = 0; done < n_frames; done += p.n_frames) {
     p.frame_begin = (int)t->frame_idx;
-    p.n_frames = std::min(chunk, n_frames - done);
+    p.n_frames = std::min(per_launch, n_frames - done);
+    // Split each pixel's frames into chunks so that the launch has about work_split items per
+    // resident lane: a persistent lane's last item is then short, and a small partition (a row
+    // band of an 8-GPU split) still fills every CU. Samples land in the per-frame buffer, so the
+    // accumulation order does not depend on the split.
+    int64_t chunks = 1;
+    if (t->work_split > 0)
+      chunks = std::max<int64_t>(1, ((int64_t)t->work_split * resident + p.tile_items - 1) / p.tile_items);
+    chunks = std::min<int64_t>(chunks, std::max<int64_t>(1, (int64_t)0x7FFFFFFF / p.tile_items));
+    chunks = std::min<int64_t>(chunks, p.n_frames);
+    p.chunk_frames = (int)((p.n_frames + chunks - 1) / chunks);
+    chunks = (p.n_frames + p.chunk_frames - 1) / p.chunk_frames;
+    p.n_items = (uint32_t)(chunks * p.tile_items);
+    p.batch_max = (uint32_t)t->batch_max;
+    p.batch_div = (uint32_t)std::max<int64_t>(1, (resident / 64) * 2);  // half of the left work / waves
+    int grid = (int)std::min<int64_t>(resident, (int64_t)p.n_items) / RenderBlockSize();
+    grid = std::max(grid, 1);
+    t->last_grid = grid;
+    t->last_chunk_frames = p.chunk_frames;
     HIP_TRY(hipMemsetAsync(t->d_work, 0, sizeof(uint32_t), t->stream));
     hipEvent_t e0 = TakeEvent(t), e1 = TakeEvent(t);
     if (e0) HIP_TRY(hipEventRecord(e0, t->stream));
     HIP_TRY(LaunchRender(p, variant, t->stats_on, grid, t->stream));
     if (e1) HIP_TRY(hipEventRecord(e1, t->stream));
     if (e0 && e1) t->pending.emplace_back(e0, e1);
+    HIP_TRY(LaunchAccumulate(t->d_samples, t->d_accum, t->d_pixels, p.local_pixels, p.n_frames,
+                             p.frame_begin + p.n_frames, t->stream));
     t->launches++;
     t->frame_idx += p.n_frames;
   }

@@ -1103,9 +1103,10 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
   const int sq = P.cam.sqrt_spp;
   const int frame_end = P.frame_begin + P.n_frames;
 
-  bool need = true;  // lane wants a pixel
+  bool need = true;  // lane wants a work item
   uint32_t lidx = 0;
-  f3 acc = mk(0, 0, 0);
+  int fstop = 0;     // end of the lane's frame chunk
+  uint32_t bnext = 0, bend = 0;  // the wave's reserved batch of work items (wave-uniform)
   uint32_t item_rays = 0;
   Path path;
   path.k0 = P.seed_lo;
@@ -1139,18 +1140,36 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
 #if RT2_EXP_STAMPS
     st_t = __builtin_amdgcn_s_memtime();
 #endif
-    // ---- hand out pixels: one atomic per wave
+    // ---- hand out work items. A wave reserves a batch [bnext, bend) with one atomic and its
+    // lanes take items from it as they finish (popcount prefix); the batch size shrinks with the
+    // work left (guided self-scheduling), so the counter sees few atomics early and the last
+    // items still spread over all waves.
     unsigned long long mask = __ballot(need);
     if (mask != 0ull) {
-      uint32_t count = (uint32_t)__popcll(mask);
-      int leader = __ffsll((long long)mask) - 1;
-      uint32_t base = 0;
-      if (lane == leader) base = atomicAdd(P.work_counter, count);
-      base = (uint32_t)__shfl((int)base, leader);
+      const uint32_t count = (uint32_t)__popcll(mask);
+      const uint32_t avail = bend - bnext;
+      const uint32_t old = bnext;
+      uint32_t fresh = 0;
+      if (count > avail) {
+        const uint32_t want = count - avail;
+        // work left as of this wave's last reservation (stale, so an overestimate)
+        const uint32_t left = P.n_items > bend ? P.n_items - bend : 0u;
+        const uint32_t size = max(want, min(P.batch_max, left / P.batch_div));
+        uint32_t b = 0;
+        if (lane == __builtin_amdgcn_readfirstlane(lane)) b = atomicAdd(P.work_counter, size);
+        fresh = __builtin_amdgcn_readfirstlane(b);
+        bnext = fresh + want;
+        bend = fresh + size;
+      } else {
+        bnext = old + count;
+      }
       if (need) {
-        uint32_t item = base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+        const uint32_t k = (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+        const uint32_t item = k < avail ? old + k : fresh + (k - avail);
         if (item >= P.n_items) break;  // no work left for this lane
-        uint32_t tile = item >> 6, within = item & 63u;
+        const uint32_t chunk = item / P.tile_items;  // chunk-major: every tile's chunk 0 first
+        const uint32_t titem = item - chunk * P.tile_items;
+        uint32_t tile = titem >> 6, within = titem & 63u;
         int x = (int)((tile % (uint32_t)P.tiles_x) * 8u + (within & 7u));
         int r = (int)((tile / (uint32_t)P.tiles_x) * 8u + (within >> 3));
         if (x >= P.width || r >= P.local_rows) continue;  // partial edge tile
@@ -1158,11 +1177,11 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
         lidx = (uint32_t)r * (uint32_t)P.width + (uint32_t)x;
         path.pix = (uint32_t)y * (uint32_t)P.width + (uint32_t)x;
         path.xy = (uint32_t)x | ((uint32_t)y << 16);
-        acc = mk(P.accum[3 * lidx], P.accum[3 * lidx + 1], P.accum[3 * lidx + 2]);
         item_rays = 0;
-        if (P.frame_begin >= frame_end) continue;  // zero frames requested
+        int f = P.frame_begin + (int)chunk * P.chunk_frames;
+        fstop = min(f + P.chunk_frames, frame_end);
+        if (f >= fstop) continue;  // zero frames requested
         need = false;
-        int f = P.frame_begin;
         path.start((uint32_t)f);
         path.sij = (uint32_t)(f % sq) | ((uint32_t)(f / sq % sq) << 16);
         camera_ray<F>(P, path, ro, rd, rtime);
@@ -1278,10 +1297,14 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
     }
     RT2_STAMP(st_shade);
     if (done) {
-      acc = acc + color;
+      // this frame's sample, summed in frame order by accumulate_kernel (RayTracer.cpp:64)
+      float* sp = P.samples + 3ull * ((unsigned long long)((int)path.frame - P.frame_begin) * P.local_pixels + lidx);
+      sp[0] = color.x;
+      sp[1] = color.y;
+      sp[2] = color.z;
       paths++;
       int f = (int)path.frame + 1;
-      if (f < frame_end) {
+      if (f < fstop) {
         path.start((uint32_t)f);
         {  // next stratum: (f % sq, f / sq % sq) from the previous frame's
           uint32_t si = (path.sij & 0xFFFFu) + 1u, sj = path.sij >> 16;
@@ -1305,22 +1328,7 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
         thr = mk(1, 1, 1);
         depth_left = P.max_depth;
       } else {
-        // RayTracer.cpp:64-66: accumulate; live display value = ToColor(clamp(accum / frame_idx, 0, 1))
-        P.accum[3 * lidx] = acc.x;
-        P.accum[3 * lidx + 1] = acc.y;
-        P.accum[3 * lidx + 2] = acc.z;
-        if (P.pixels) {
-          f3 c = acc / (float)frame_end;
-          float cc[3] = {c.x, c.y, c.z};
-          uint32_t rgba = 0xFF000000u;
-#pragma unroll
-          for (int k = 0; k < 3; k++) {
-            float v = gmin(gmax(cc[k], 0.0f), 1.0f);
-            rgba |= ((uint32_t)(uint8_t)floor((double)v * 255.999)) << (8 * k);
-          }
-          reinterpret_cast<uint32_t*>(P.pixels)[lidx] = rgba;
-        }
-        if (P.ray_counts) P.ray_counts[lidx] += item_rays;
+        if (P.ray_counts) atomicAdd(P.ray_counts + lidx, item_rays);
         rays += item_rays;
         need = true;
       }
@@ -1350,6 +1358,58 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
 #if RT2_EXP_WAVESTEPS
   for (int k = 0; k < 8; k++) atomicAdd(P.stats + StatsCounters::kDiag + k, (unsigned long long)cnt.wd[k]);
 #endif
+}
+
+// ------------------------------------------------------------------------------------------
+// RayTracer.cpp:64-66 for a launch's frames: accum[i] += sample(f) in frame order (the float sum
+// of the reference's per-Update accumulation, bit for bit), then the live display value
+// pixels[i] = ToColor(clamp(accum[i] / frame_idx, 0, 1)). One thread per local pixel; a frame's
+// samples are pixel-contiguous, so every load is coalesced and the kernel streams the sample
+// buffer once at HBM rate.
+__global__ __launch_bounds__(256) void accumulate_kernel(const float* __restrict__ samples, float* __restrict__ accum,
+                                                         uint32_t* __restrict__ pixels, uint32_t npix, int n_frames,
+                                                         int frame_idx) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= npix) return;
+  float a0 = accum[3 * i], a1 = accum[3 * i + 1], a2 = accum[3 * i + 2];
+  const float* s = samples + 3ull * i;
+  const unsigned long long stride = 3ull * npix;
+  int f = 0;
+  for (; f + 4 <= n_frames; f += 4) {  // four frames' loads in flight, summed in order
+    float x[4][3];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      x[k][0] = s[k * stride];
+      x[k][1] = s[k * stride + 1];
+      x[k][2] = s[k * stride + 2];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      a0 += x[k][0];
+      a1 += x[k][1];
+      a2 += x[k][2];
+    }
+    s += 4 * stride;
+  }
+  for (; f < n_frames; f++, s += stride) {
+    a0 += s[0];
+    a1 += s[1];
+    a2 += s[2];
+  }
+  accum[3 * i] = a0;
+  accum[3 * i + 1] = a1;
+  accum[3 * i + 2] = a2;
+  if (pixels) {
+    const float fi = (float)frame_idx;
+    const float cc[3] = {a0 / fi, a1 / fi, a2 / fi};
+    uint32_t rgba = 0xFF000000u;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      float v = gmin(gmax(cc[k], 0.0f), 1.0f);
+      rgba |= ((uint32_t)(uint8_t)floor((double)v * 255.999)) << (8 * k);
+    }
+    pixels[i] = rgba;
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1468,6 +1528,14 @@ hipError_t LaunchRender(const RenderParams& p, int variant, bool stats, int grid
   dev::KernelFn fn = dev::Kernel(variant, RenderMode(p), stats);
   if (!fn) return hipErrorInvalidValue;
   hipLaunchKernelGGL(fn, dim3(grid), dim3(dev::kBlock), RenderLdsBytes(p), stream, p);
+  return hipGetLastError();
+}
+
+hipError_t LaunchAccumulate(const float* samples, float* accum, uint8_t* pixels, uint32_t npix, int n_frames,
+                            int frame_idx, hipStream_t stream) {
+  if (npix == 0) return hipSuccess;
+  hipLaunchKernelGGL(dev::accumulate_kernel, dim3((npix + 255u) / 256u), dim3(256), 0, stream, samples, accum,
+                     reinterpret_cast<uint32_t*>(pixels), npix, n_frames, frame_idx);
   return hipGetLastError();
 }
 

@@ -150,12 +150,16 @@ struct RenderParams {
   int local_rows;          // rows owned by this rank
   int band_h, rank, world; // interleaved row bands: global band b -> rank b % world
   int tiles_x;             // ceil(width / 8)
-  uint32_t n_items;        // tiles_x * ceil(local_rows / 8) * 64
+  uint32_t tile_items;     // tiles_x * ceil(local_rows / 8) * 64: lanes of one frame chunk
+  uint32_t n_items;        // tile_items * chunks (work item = one pixel x one chunk of frames)
+  uint32_t batch_max;      // most work items a wave reserves at once
+  uint32_t batch_div;      // a wave reserves (items left) / batch_div, at least what it needs
   int frame_begin, n_frames, max_depth;
+  int chunk_frames;        // frames per work item; chunk c = [frame_begin + c*chunk_frames, ...)
   uint32_t seed_lo, seed_hi;
-  float* accum;            // float3 per local pixel (row-major local rows)
-  uint8_t* pixels;         // RGBA8 per local pixel (RayTracer::Pixels)
-  uint32_t* ray_counts;    // optional: += rays per local pixel
+  float* samples;          // float3 per (launch frame, local pixel): [n_frames][local pixels][3]
+  uint32_t local_pixels;   // width * local_rows
+  uint32_t* ray_counts;    // optional: += rays per local pixel (atomic: chunks of a pixel overlap)
   uint32_t* work_counter;  // zeroed before launch
   unsigned long long* stats;  // StatsCounters::kCount slots
   int stack_depth;         // traversal-stack entries per lane (<= kTraversalStack)

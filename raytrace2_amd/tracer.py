@@ -271,6 +271,20 @@ class RayTracer:
     def set_launch_frames(self, n: int) -> None:
         check(lib.rt2_tracer_set_launch_frames(self._h, int(n)))
 
+    def set_work_split(self, items_per_lane: int) -> None:
+        check(lib.rt2_tracer_set_work_split(self._h, int(items_per_lane)))
+
+    def set_sample_budget(self, nbytes: int) -> None:
+        check(lib.rt2_tracer_set_sample_budget(self._h, int(nbytes)))
+
+    def set_batch_max(self, items: int) -> None:
+        check(lib.rt2_tracer_set_batch_max(self._h, int(items)))
+
+    def last_launch(self) -> dict:
+        g, c, v = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        check(lib.rt2_tracer_last_launch(self._h, ctypes.byref(g), ctypes.byref(c), ctypes.byref(v)))
+        return {"grid": g.value, "chunk_frames": c.value, "variant": v.value}
+
     def set_stream(self, hip_stream_ptr: Optional[int]) -> None:
         check(lib.rt2_tracer_set_stream(self._h, ctypes.c_void_p(hip_stream_ptr or None)))
 

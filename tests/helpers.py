@@ -7,7 +7,7 @@ SEED = 0x5EED2024
 
 
 def gpu_render(name, w, h, spp, frames, *, seed=SEED, max_depth=50, band_h=0, rank=0, world=1,
-               launch_frames=0, updates=False, stats=False):
+               launch_frames=0, updates=False, stats=False, work_split=None, sample_budget=None, batch_max=None):
     import torch  # noqa: F401
     import raytrace2_amd as R
     sc = R.Scene(scene_path(name), seed)
@@ -23,6 +23,12 @@ def gpu_render(name, w, h, spp, frames, *, seed=SEED, max_depth=50, band_h=0, ra
         tr.set_partition(band_h, rank, world)
     if launch_frames:
         tr.set_launch_frames(launch_frames)
+    if work_split is not None:
+        tr.set_work_split(work_split)
+    if sample_budget is not None:
+        tr.set_sample_budget(sample_budget)
+    if batch_max is not None:
+        tr.set_batch_max(batch_max)
     if updates:
         for _ in range(frames):
             tr.Update(sc)

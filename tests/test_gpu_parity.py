@@ -63,6 +63,32 @@ def test_update_equals_render_and_chunking(have_gpu):
     assert np.array_equal(r1, r2) and np.array_equal(r1, r3)
 
 
+@pytest.mark.parametrize("name", ["cornell_box_original", "final_render_book_1"])
+def test_work_split_is_invisible(have_gpu, name):
+    # A pixel's frames cut into chunks rendered by different lanes (any chunk size, any wave batch,
+    # several launches when the sample buffer is small) must sum to the same bits: samples are
+    # accumulated in frame order after each launch (RayTracer.cpp:64).
+    w, h, spp, frames = 72, 40, 64, 13
+    base = gpu_render(name, w, h, spp, frames, work_split=0)
+    o_acc, o_rc, _ = oracle_render(name, w, h, spp, frames, forward=True)
+    assert np.array_equal(base[0].view(np.uint32), o_acc.view(np.uint32))
+    assert np.array_equal(base[1], o_rc)
+    frame_bytes = w * h * 12
+    for kw in (dict(work_split=1), dict(work_split=100000), dict(work_split=64, batch_max=1),
+               dict(work_split=64, batch_max=4096), dict(sample_budget=3 * frame_bytes),
+               dict(sample_budget=1, work_split=5), dict(launch_frames=4, sample_budget=2 * frame_bytes)):
+        acc, rc, st, px = gpu_render(name, w, h, spp, frames, **kw)
+        assert np.array_equal(acc.view(np.uint32), base[0].view(np.uint32)), kw
+        assert np.array_equal(rc, base[1]), kw
+        assert np.array_equal(px, base[3]), kw
+    # a larger image, where a small split gives multi-frame chunks of uneven length
+    big = gpu_render(name, 256, 256, spp, frames, work_split=0)
+    for split in (1, 2, 3):
+        acc, rc, _, _ = gpu_render(name, 256, 256, spp, frames, work_split=split)
+        assert np.array_equal(acc.view(np.uint32), big[0].view(np.uint32)), split
+        assert np.array_equal(rc, big[1]), split
+
+
 def test_row_band_partition_reassembles_bitwise(have_gpu):
     import raytrace2_amd as R
     w, h = 50, 45
