@@ -66,9 +66,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # RT2_BENCH_BACKEND=gloo + RT2_BENCH_SHARE_GPU=1: rehearsal of the N-rank flow with every rank
+    # on GPU 0 and the gather over gloo through host memory (the real run is RCCL, one GPU per rank)
+    backend = os.environ.get("RT2_BENCH_BACKEND", "nccl")
+    if os.environ.get("RT2_BENCH_SHARE_GPU") == "1":
+        local_rank = 0
     if world > 1:
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
 
@@ -101,14 +109,19 @@ def main():
     setup_s = time.perf_counter() - t0
     rows = tr.local_rows()
     from raytrace2_amd.dist import BandGather
-    gath = BandGather(a.height, a.width, a.band_h, world, rank, dev) if emulate == 1 else None
+    host_gather = world > 1 and backend != "nccl"
+    gath = (BandGather(a.height, a.width, a.band_h, world, rank, torch.device("cpu") if host_gather else dev)
+            if emulate == 1 else None)
     assert gath is None or gath.local_view().shape[0] == rows
 
     def step():
         tr.Reset()
         tr.Render(a.spp)
         if gath is not None:
-            tr.copy_accum_to(gath.send.data_ptr(), stream.cuda_stream)
+            if host_gather:
+                gath.local_view().copy_(torch.from_numpy(tr.Accumulation()))
+            else:
+                tr.copy_accum_to(gath.send.data_ptr(), stream.cuda_stream)
             gath.gather()  # RCCL gather of the row bands to rank 0 + de-interleave
 
     for _ in range(a.warmup):
@@ -136,7 +149,7 @@ def main():
     kernel_ms = st["kernel_ms"]
     launches = max(1, st["launches"])
     if world > 1:
-        t = torch.tensor([elapsed, float(rays_local)], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, float(rays_local)], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         tmax = t.clone()
         dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
         dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)

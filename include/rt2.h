@@ -99,7 +99,7 @@ RT2_API int rt2_settings_load(const char* path, rt2_app_settings* out);
 RT2_API int rt2_tracer_create(const rt2_scene* scene, int device, rt2_tracer** out);
 RT2_API void rt2_tracer_destroy(rt2_tracer* tr);
 RT2_API int rt2_tracer_set_stream(rt2_tracer* tr, void* hip_stream); /* NULL = own stream */
-RT2_API int rt2_tracer_set_max_depth(rt2_tracer* tr, int max_depth); /* RayTracer::max_depth */
+RT2_API int rt2_tracer_set_max_depth(rt2_tracer* tr, int max_depth); /* RayTracer::max_depth, <= 65535 */
 RT2_API int rt2_tracer_set_samples_per_pixel(rt2_tracer* tr, int spp); /* App.cpp:129 */
 RT2_API int rt2_tracer_set_seed(rt2_tracer* tr, uint64_t seed);
 RT2_API int rt2_tracer_set_partition(rt2_tracer* tr, int band_h, int rank, int world);

@@ -80,6 +80,7 @@ struct rt2_tracer {
   int last_variant = -1;
   int last_grid = 0;
   uint64_t launches = 0;
+  uint64_t paths = 0;
   double kernel_ms = 0;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;  // per-launch timing events
   std::vector<hipEvent_t> event_pool;
@@ -457,7 +458,9 @@ int rt2_tracer_set_stream(rt2_tracer* t, void* s) {
 
 int rt2_tracer_set_max_depth(rt2_tracer* t, int d) {
   if (!t) return Fail(RT2_ERR_INVALID, "null tracer");
-  t->max_depth = d;
+  // RayTracer::max_depth is a size_t (RayTracer.hpp:32); the kernel keeps it in 16 bits
+  if (d > 0xFFFF) return Fail(RT2_ERR_INVALID, "max_depth must be at most 65535");
+  t->max_depth = d < 0 ? 0 : d;
   return RT2_OK;
 }
 
@@ -577,7 +580,10 @@ int rt2_tracer_render(rt2_tracer* t, int n_frames) {
   p.lin_len = t->use_linear ? t->lin_len : 0u;
   uint32_t feats = t->features | (p.cam.defocus_angle > 0.0f ? (uint32_t)kFeatDefocus : 0u);
   int variant = RenderVariant(feats);
-  const int64_t resident = (int64_t)t->cus * RenderBlocksPerCU(variant, RenderMode(p), t->stats_on,
+  // per-record counters and per-pixel ray counts come from the counting kernel instantiation (same
+  // arithmetic, extra counters); the product kernel keeps only the wave ray totals
+  const bool counting = t->stats_on || t->ray_counts_on;
+  const int64_t resident = (int64_t)t->cus * RenderBlocksPerCU(variant, RenderMode(p), counting,
                                                                  RenderLdsBytes(p)) * RenderBlockSize();
   // frames per launch: the caller's launch_frames, bounded by the sample-buffer budget
   const size_t frame_bytes = (size_t)p.local_pixels * 3 * sizeof(float);
@@ -606,6 +612,7 @@ int rt2_tracer_render(rt2_tracer* t, int n_frames) {
       chunks = std::max<int64_t>(1, ((int64_t)t->work_split * resident + p.tile_items - 1) / p.tile_items);
     chunks = std::min<int64_t>(chunks, std::max<int64_t>(1, (int64_t)0x7FFFFFFF / p.tile_items));
     chunks = std::min<int64_t>(chunks, p.n_frames);
+    chunks = std::max<int64_t>(chunks, ((int64_t)p.n_frames + 0xFFFF) / 0x10000);  // kernel: <= 2^16 frames per item
     p.chunk_frames = (int)((p.n_frames + chunks - 1) / chunks);
     chunks = (p.n_frames + p.chunk_frames - 1) / p.chunk_frames;
     p.n_items = (uint32_t)(chunks * p.tile_items);
@@ -618,12 +625,13 @@ int rt2_tracer_render(rt2_tracer* t, int n_frames) {
     HIP_TRY(hipMemsetAsync(t->d_work, 0, sizeof(uint32_t), t->stream));
     hipEvent_t e0 = TakeEvent(t), e1 = TakeEvent(t);
     if (e0) HIP_TRY(hipEventRecord(e0, t->stream));
-    HIP_TRY(LaunchRender(p, variant, t->stats_on, grid, t->stream));
+    HIP_TRY(LaunchRender(p, variant, counting, grid, t->stream));
     if (e1) HIP_TRY(hipEventRecord(e1, t->stream));
     if (e0 && e1) t->pending.emplace_back(e0, e1);
     HIP_TRY(LaunchAccumulate(t->d_samples, t->d_accum, t->d_pixels, p.local_pixels, p.n_frames,
                              p.frame_begin + p.n_frames, t->stream));
     t->launches++;
+    t->paths += (uint64_t)p.n_frames * p.local_pixels;
     t->frame_idx += p.n_frames;
   }
   if (t->pending.size() > 256) return DrainEvents(t);
@@ -723,7 +731,7 @@ int rt2_tracer_get_stats(rt2_tracer* t, rt2_stats* o) {
   unsigned long long s[kStatsSlots];
   HIP_TRY(hipMemcpy(s, t->d_stats, sizeof(s), hipMemcpyDeviceToHost));
   o->rays = s[StatsCounters::kRays];
-  o->paths = s[StatsCounters::kPaths];
+  o->paths = t->paths;  // every (pixel, frame) of a launch finishes exactly one camera path
   o->bvh_tests = s[StatsCounters::kBvhTests];
   o->quad_tests = s[StatsCounters::kQuadTests];
   o->sphere_tests = s[StatsCounters::kSphereTests];
@@ -763,6 +771,7 @@ int rt2_tracer_reset_stats(rt2_tracer* t) {
   if (rc != RT2_OK) return rc;
   HIP_TRY(hipMemset(t->d_stats, 0, kStatsSlots * sizeof(unsigned long long)));
   t->launches = 0;
+  t->paths = 0;
   t->kernel_ms = 0;
   return RT2_OK;
 }

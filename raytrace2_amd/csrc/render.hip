@@ -227,7 +227,8 @@ __device__ __forceinline__ float to_unit(uint32_t v) { return (float)(v >> 8) * 
 
 // The per-lane path context the samplers need.
 struct Path {
-  uint32_t k0, k1, pix, frame;
+  uint32_t k0, k1, width;  // wave-uniform: seed, image width
+  uint32_t frame;
   uint32_t xy;   // pixel x | y << 16 (global image coordinates)
   uint32_t sij;  // stratum s_i | s_j << 16 of `frame` (RayTracer.cpp:59-60), advanced per frame
   uint32_t n;
@@ -245,7 +246,7 @@ struct Path {
 #pragma unroll
     for (int j = 0; j < K; j++) v[j] = sel4((i + (uint32_t)j) & 3u, r0, r1, r2, r3);
     if (fresh || i + (uint32_t)K > 4u) {
-      philox(k0, k1, pix, frame, (n >> 2) + (fresh ? 0u : 1u), r0, r1, r2, r3);
+      philox(k0, k1, (xy >> 16) * width + (xy & 0xFFFFu), frame, (n >> 2) + (fresh ? 0u : 1u), r0, r1, r2, r3);
 #pragma unroll
       for (int j = 0; j < K; j++)
         if (fresh || i + (uint32_t)j >= 4u) v[j] = sel4((i + (uint32_t)j) & 3u, r0, r1, r2, r3);
@@ -1075,6 +1076,20 @@ __device__ __forceinline__ void camera_ray(const RenderParams& P, Path& g, f3& o
   d = normalize(pc - c);
 }
 
+// Local (row-band) pixel index of global pixel xy: global row y belongs to band y / band_h, owned by
+// rank (y / band_h) % world and stored as local row (y / (band_h * world)) * band_h + y % band_h.
+__device__ __forceinline__ uint32_t local_index(const RenderParams& P, uint32_t xy) {
+  const uint32_t x = xy & 0xFFFFu, y = xy >> 16;
+  uint32_t r = y;
+  if (P.world > 1) {
+    uint32_t bh = (uint32_t)P.band_h, bw = bh * (uint32_t)P.world;
+    asm volatile("" : "+s"(bh), "+s"(bw));  // per-call reciprocals (see camera_ray)
+    const uint32_t q = y / bw;
+    r = q * bh + (y - (y / bh) * bh);
+  }
+  return r * (uint32_t)P.width + x;
+}
+
 // Occupancy target (waves per SIMD the register allocation must allow) for the threaded-traversal
 // product kernels: the highest that compiles without VGPR spills. Stack-traversal and stats
 // kernels keep the compiler's own allocation (their LDS stack bounds occupancy anyway).
@@ -1082,7 +1097,7 @@ template <uint32_t F, int kMode, bool kStats>
 constexpr int MinWaves() {
   if (RT2_MIN_WAVES_PER_EU > 0) return RT2_MIN_WAVES_PER_EU;
   if (kStats || kMode != kModeLinear) return 1;
-  if (F == kFeatXform) return 6;                  // Cornell: 80 VGPRs
+  if (F == kFeatXform) return 7;                  // Cornell: 72 VGPRs
   if (F == (kFeatXform | kFeatMedium)) return 5;  // Cornell volume: 95 VGPRs
   if (F == kFeatAll) return 1;
   return 6;                                       // book 1
@@ -1100,27 +1115,26 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
   const int lane = (int)__lane_id();
   const float4* M = reinterpret_cast<const float4*>(P.materials);
   const f3 bg = mk(P.background[0], P.background[1], P.background[2]);
-  const int sq = P.cam.sqrt_spp;
   const int frame_end = P.frame_begin + P.n_frames;
-
-  bool need = true;  // lane wants a work item
-  uint32_t lidx = 0;
-  int fstop = 0;     // end of the lane's frame chunk
+  bool need = true;   // lane wants a work item
+  bool idle = false;  // no work left for this lane: it stays in the loop, masked, until the wave ends,
+                      // so the loop head is a convergence point and wave totals stay in SGPRs
+  unsigned long long rays = 0;  // rays cast by the wave (popcounts of a ballot at the loop head)
   uint32_t bnext = 0, bend = 0;  // the wave's reserved batch of work items (wave-uniform)
   uint32_t item_rays = 0;
   Path path;
   path.k0 = P.seed_lo;
   path.k1 = P.seed_hi;
-  path.pix = 0;
+  path.width = (uint32_t)P.width;
   path.xy = 0;
-  path.sij = 0;
   path.start(0);
   path.r0 = path.r1 = path.r2 = path.r3 = 0;
   f3 ro = mk(0, 0, 0), rd = mk(0, 0, 1), thr = mk(1, 1, 1);
   float rtime = 0.0f;
-  int depth_left = 0;
+  // depth_left (RayColor's depth, low 16 bits) | frames of the lane's chunk after this one (high 16)
+  uint32_t dl = 0;
+  const uint32_t max_depth = (uint32_t)P.max_depth;  // <= 0xFFFF (rt2_tracer_set_max_depth)
   Counters cnt = {};
-  uint32_t rays = 0, paths = 0;
   bool overflow = false;
 
 #if RT2_EXP_STAMPS
@@ -1144,7 +1158,7 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
     // lanes take items from it as they finish (popcount prefix); the batch size shrinks with the
     // work left (guided self-scheduling), so the counter sees few atomics early and the last
     // items still spread over all waves.
-    unsigned long long mask = __ballot(need);
+    unsigned long long mask = __ballot(need && !idle);
     if (mask != 0ull) {
       const uint32_t count = (uint32_t)__popcll(mask);
       const uint32_t avail = bend - bnext;
@@ -1163,42 +1177,52 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
       } else {
         bnext = old + count;
       }
-      if (need) {
+      if (need && !idle) {
         const uint32_t k = (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
         const uint32_t item = k < avail ? old + k : fresh + (k - avail);
-        if (item >= P.n_items) break;  // no work left for this lane
-        const uint32_t chunk = item / P.tile_items;  // chunk-major: every tile's chunk 0 first
-        const uint32_t titem = item - chunk * P.tile_items;
-        uint32_t tile = titem >> 6, within = titem & 63u;
-        int x = (int)((tile % (uint32_t)P.tiles_x) * 8u + (within & 7u));
-        int r = (int)((tile / (uint32_t)P.tiles_x) * 8u + (within >> 3));
-        if (x >= P.width || r >= P.local_rows) continue;  // partial edge tile
-        int y = ((r / P.band_h) * P.world + P.rank) * P.band_h + (r % P.band_h);
-        lidx = (uint32_t)r * (uint32_t)P.width + (uint32_t)x;
-        path.pix = (uint32_t)y * (uint32_t)P.width + (uint32_t)x;
-        path.xy = (uint32_t)x | ((uint32_t)y << 16);
-        item_rays = 0;
-        int f = P.frame_begin + (int)chunk * P.chunk_frames;
-        fstop = min(f + P.chunk_frames, frame_end);
-        if (f >= fstop) continue;  // zero frames requested
-        need = false;
-        path.start((uint32_t)f);
-        path.sij = (uint32_t)(f % sq) | ((uint32_t)(f / sq % sq) << 16);
-        camera_ray<F>(P, path, ro, rd, rtime);
-        thr = mk(1, 1, 1);
-        depth_left = P.max_depth;
+        // (no `continue` here: every lane reaches the loop-head ballots below)
+        if (item >= P.n_items) {
+          idle = true;  // no work left for this lane
+        } else {
+          const uint32_t chunk = item / P.tile_items;  // chunk-major: every tile's chunk 0 first
+          const uint32_t titem = item - chunk * P.tile_items;
+          uint32_t tile = titem >> 6, within = titem & 63u;
+          int x = (int)((tile % (uint32_t)P.tiles_x) * 8u + (within & 7u));
+          int r = (int)((tile / (uint32_t)P.tiles_x) * 8u + (within >> 3));
+          int f = P.frame_begin + (int)chunk * P.chunk_frames;
+          const int fstop = min(f + P.chunk_frames, frame_end);  // chunk_frames <= 0x10000
+          if (x < P.width && r < P.local_rows && f < fstop) {  // else: partial edge tile, or no frames
+            int y = ((r / P.band_h) * P.world + P.rank) * P.band_h + (r % P.band_h);
+            path.xy = (uint32_t)x | ((uint32_t)y << 16);
+            item_rays = 0;
+            need = false;
+            path.start((uint32_t)f);
+            {  // stratum (RayTracer.cpp:59-60): s_i = f % sq, s_j = (f / sq) % sq; then advanced per frame
+              // (divisor opaque here: a reciprocal hoisted out of the render loop would hold a VGPR)
+              uint32_t sq = (uint32_t)P.cam.sqrt_spp;
+              asm volatile("" : "+s"(sq));
+              const uint32_t fq = (uint32_t)f / sq;
+              path.sij = ((uint32_t)f - fq * sq) | ((fq % sq) << 16);
+            }
+            camera_ray<F>(P, path, ro, rd, rtime);
+            thr = mk(1, 1, 1);
+            dl = max_depth | ((uint32_t)(fstop - f - 1) << 16);
+          }
+        }
       }
     }
+    if (__ballot(!idle) == 0ull) break;  // the wave is done (uniform exit)
+    rays += (unsigned long long)__popcll(__ballot(!need && (dl & 0xFFFFu) != 0u));  // RayColor casts below
     if (need) continue;
     RT2_STAMP(st_fetch);
 
     // ---- one bounce (RayColor, RayTracer.cpp:20-45)
     bool done = false;
     f3 color = mk(0, 0, 0);
-    if (depth_left <= 0) {
+    if ((dl & 0xFFFFu) == 0u) {
       done = true;  // RayColor(depth <= 0) returns 0 without casting a ray
     } else {
-      item_rays++;
+      if constexpr (kStats) item_rays++;
       HitRef h;
       bool hit;
       if constexpr (kMode == kModeLinear) {
@@ -1291,26 +1315,27 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
           thr = thr * att;
           ro = hp;
           rd = dir;
-          depth_left--;
+          dl--;  // depth_left > 0 here: no borrow into the frame count
         }
       }
     }
     RT2_STAMP(st_shade);
     if (done) {
       // this frame's sample, summed in frame order by accumulate_kernel (RayTracer.cpp:64)
+      const uint32_t lidx = local_index(P, path.xy);
       float* sp = P.samples + 3ull * ((unsigned long long)((int)path.frame - P.frame_begin) * P.local_pixels + lidx);
       sp[0] = color.x;
       sp[1] = color.y;
       sp[2] = color.z;
-      paths++;
       int f = (int)path.frame + 1;
-      if (f < fstop) {
+      if (dl >> 16) {
         path.start((uint32_t)f);
         {  // next stratum: (f % sq, f / sq % sq) from the previous frame's
+          const uint32_t sq = (uint32_t)P.cam.sqrt_spp;
           uint32_t si = (path.sij & 0xFFFFu) + 1u, sj = path.sij >> 16;
-          if (si == (uint32_t)sq) {
+          if (si == sq) {
             si = 0u;
-            sj = sj + 1u == (uint32_t)sq ? 0u : sj + 1u;
+            sj = sj + 1u == sq ? 0u : sj + 1u;
           }
           path.sij = si | (sj << 16);
         }
@@ -1326,10 +1351,9 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
 #endif
         camera_ray<F>(P, path, ro, rd, rtime);
         thr = mk(1, 1, 1);
-        depth_left = P.max_depth;
+        dl = ((dl & 0xFFFF0000u) - 0x10000u) | max_depth;
       } else {
-        if (P.ray_counts) atomicAdd(P.ray_counts + lidx, item_rays);
-        rays += item_rays;
+        if (kStats && P.ray_counts) atomicAdd(P.ray_counts + lidx, item_rays);
         need = true;
       }
     }
@@ -1344,8 +1368,7 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
     atomicAdd(P.stats + StatsCounters::kStamps + 3, st_finish);
   }
 #endif
-  atomicAdd(P.stats + StatsCounters::kRays, (unsigned long long)rays);
-  atomicAdd(P.stats + StatsCounters::kPaths, (unsigned long long)paths);
+  if (lane == 0) atomicAdd(P.stats + StatsCounters::kRays, rays);
   if (kStats) {
     atomicAdd(P.stats + StatsCounters::kBvhTests, (unsigned long long)cnt.bvh);
     atomicAdd(P.stats + StatsCounters::kQuadTests, (unsigned long long)cnt.quad);

@@ -6,8 +6,8 @@ from conftest import scene_path
 SEED = 0x5EED2024
 
 
-def gpu_render(name, w, h, spp, frames, *, seed=SEED, max_depth=50, band_h=0, rank=0, world=1,
-               launch_frames=0, updates=False, stats=False, work_split=None, sample_budget=None, batch_max=None):
+def _gpu_render_once(name, w, h, spp, frames, *, seed, max_depth, band_h, rank, world, launch_frames, updates,
+                     stats, work_split, sample_budget, batch_max, ray_counts):
     import torch  # noqa: F401
     import raytrace2_amd as R
     sc = R.Scene(scene_path(name), seed)
@@ -15,7 +15,8 @@ def gpu_render(name, w, h, spp, frames, *, seed=SEED, max_depth=50, band_h=0, ra
     tr.set_seed(seed)
     tr.SetSamplesPerPixel(spp)
     tr.max_depth = max_depth
-    tr.enable_ray_counts(True)
+    if ray_counts:
+        tr.enable_ray_counts(True)
     if stats:
         tr.enable_stats(True)
     tr.OnResize((w, h))
@@ -35,10 +36,29 @@ def gpu_render(name, w, h, spp, frames, *, seed=SEED, max_depth=50, band_h=0, ra
     else:
         tr.Render(frames)
     acc = tr.Accumulation()
-    rc = tr.ray_counts()
+    rc = tr.ray_counts() if ray_counts else None
     st = tr.stats()
     px = tr.Pixels()
     tr.close()
+    return acc, rc, st, px
+
+
+def gpu_render(name, w, h, spp, frames, *, seed=SEED, max_depth=50, band_h=0, rank=0, world=1,
+               launch_frames=0, updates=False, stats=False, work_split=None, sample_budget=None, batch_max=None,
+               counts=True):
+    """Renders with the product kernel (no per-pixel counters) and, when `counts`, again with the
+    counting kernel (per-pixel ray counts); the two must agree bit for bit. Returns the product
+    render's (accumulation, ray counts of the counting render or None, stats, pixels)."""
+    kw = dict(seed=seed, max_depth=max_depth, band_h=band_h, rank=rank, world=world, launch_frames=launch_frames,
+              updates=updates, work_split=work_split, sample_budget=sample_budget, batch_max=batch_max)
+    acc, _, st, px = _gpu_render_once(name, w, h, spp, frames, stats=stats, ray_counts=False, **kw)
+    rc = None
+    if counts:
+        acc2, rc, st2, px2 = _gpu_render_once(name, w, h, spp, frames, stats=True, ray_counts=True, **kw)
+        assert np.array_equal(acc.view(np.uint32), acc2.view(np.uint32)), "product and counting kernels differ"
+        assert np.array_equal(px, px2)
+        assert st["rays"] == st2["rays"] == int(rc.astype(np.uint64).sum()), (st["rays"], st2["rays"])
+        assert st["paths"] == st2["paths"]
     return acc, rc, st, px
 
 
