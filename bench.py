@@ -83,6 +83,12 @@ def main():
     import raytrace2_amd as R
 
     scene_file = os.path.join(ROOT, "scenes", a.scene)
+    if a.scene.startswith("gen:"):  # gen:<generator>:<n>:<seed> -> raytrace2_amd.authoring scene
+        import random
+        from raytrace2_amd import authoring
+        _, gen, n, gseed = a.scene.split(":")
+        scene_file = f"/tmp/rt2_{gen}_{n}_{gseed}.json"
+        authoring.GENERATORS[gen](random.Random(int(gseed)), int(n)).dump(scene_file)
     t0 = time.perf_counter()
     sc = R.Scene(scene_file, a.seed)
     tr = R.RayTracer(sc, local_rank)

@@ -160,3 +160,17 @@ def test_list_acceleration_matches_linear_child_loop(have_gpu, monkeypatch):
     mism = np.count_nonzero(a1.view(np.uint32) != a2.view(np.uint32))
     assert mism == 0, f"{mism} floats differ"
     assert s1["sphere_tests"] * 5 < s2["sphere_tests"], (s1["sphere_tests"], s2["sphere_tests"])
+
+
+def test_generated_stress_scene(have_gpu, tmp_path):
+    """A scene from the authoring module (3000 random spheres: stack traversal over a global-memory
+    scene) is bit-identical to the oracle too."""
+    import random
+    from raytrace2_amd import authoring as A
+    p = str(tmp_path / "field.json")
+    A.sphere_field(3000, random.Random(1)).dump(p)
+    acc, rc, st, _ = gpu_render(p, 64, 36, 64, 4)
+    o_acc, o_rc, o_cnt = oracle_render(p, 64, 36, 64, 4, forward=True)
+    assert st["overflow"] == 0
+    np.testing.assert_array_equal(rc, o_rc)
+    assert np.array_equal(acc.view(np.uint32), o_acc.view(np.uint32))
