@@ -95,7 +95,11 @@ RT2_API int rt2_settings_load(const char* path, rt2_app_settings* out);
  * on_resize:OnResize(dims) (RayTracer.cpp:87-104): sets camera dims, reallocates, Reset().
  * update:   Update(scene) (RayTracer.cpp:55-70): one frame, stratum (f % sq, f / sq % sq).
  * render:   n consecutive Update() calls, executed as ceil(n / launch_frames) kernel launches.
- * Frames are enqueued on the tracer's stream; readbacks synchronise it. */
+ * Update()/render() queue their frames; queued frames are launched together at the next readback,
+ * query, synchronize or stats call, before a change of max_depth / spp / seed / stats mode, or once
+ * `lazy_frames` (default 4096; 0 = launch at every call) are queued. Reset/OnResize drop queued
+ * frames. Results are identical either way; FrameIdx() counts queued frames. Launched frames run on
+ * the tracer's stream; readbacks synchronise it. */
 RT2_API int rt2_tracer_create(const rt2_scene* scene, int device, rt2_tracer** out);
 RT2_API void rt2_tracer_destroy(rt2_tracer* tr);
 RT2_API int rt2_tracer_set_stream(rt2_tracer* tr, void* hip_stream); /* NULL = own stream */
@@ -109,6 +113,7 @@ RT2_API int rt2_tracer_set_launch_frames(rt2_tracer* tr, int frames_per_launch);
  * per pixel). Every frame's sample goes to a per-frame buffer and is summed in frame order after
  * the launch, so results do not depend on the split. The buffer is bounded by `bytes` (default
  * 16 GiB): a render needing more runs as several launches. */
+RT2_API int rt2_tracer_set_lazy_frames(rt2_tracer* tr, int max_queued);
 RT2_API int rt2_tracer_set_work_split(rt2_tracer* tr, int items_per_lane);
 RT2_API int rt2_tracer_set_sample_budget(rt2_tracer* tr, uint64_t bytes);
 /* Most work items a GPU wave reserves with one atomic (default 64); batches shrink as the launch
@@ -128,6 +133,14 @@ RT2_API int rt2_tracer_local_rows(const rt2_tracer* tr);
 RT2_API int rt2_tracer_non_converted_pixels(rt2_tracer* tr, float* out);
 RT2_API int rt2_tracer_accumulation(rt2_tracer* tr, float* out); /* raw float3 sums */
 RT2_API int rt2_tracer_pixels(rt2_tracer* tr, uint8_t* out_rgba); /* Pixels(): RGBA8 */
+/* Progressive display (App.cpp:176-242 without the window): enqueue the Pixels() readback after the
+ * frames already enqueued and return at once; the buffer is complete when rt2_tracer_query returns
+ * 1 (all enqueued work done; 0 = still running) or after rt2_tracer_synchronize. Pinned host memory
+ * from rt2_host_alloc makes the copy a DMA that does not stall the host. */
+RT2_API int rt2_tracer_pixels_async(rt2_tracer* tr, uint8_t* out_rgba);
+RT2_API int rt2_tracer_query(rt2_tracer* tr);
+RT2_API int rt2_host_alloc(size_t bytes, void** out);
+RT2_API void rt2_host_free(void* ptr);
 /* Device-to-device copy of the local accumulation (float3 per local pixel) into `dst_device`,
  * ordered on `hip_stream` (NULL = tracer stream) — used for the multi-GPU gather. */
 RT2_API int rt2_tracer_copy_accum_device(rt2_tracer* tr, void* dst_device, void* hip_stream);

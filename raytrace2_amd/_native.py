@@ -106,9 +106,14 @@ def _load():
         "rt2_tracer_set_seed": (i32, [vp, u64]),
         "rt2_tracer_set_partition": (i32, [vp, i32, i32, i32]),
         "rt2_tracer_set_launch_frames": (i32, [vp, i32]),
+        "rt2_tracer_set_lazy_frames": (i32, [vp, i32]),
         "rt2_tracer_set_work_split": (i32, [vp, i32]),
         "rt2_tracer_set_sample_budget": (i32, [vp, u64]),
         "rt2_tracer_set_batch_max": (i32, [vp, i32]),
+        "rt2_tracer_pixels_async": (i32, [vp, ctypes.POINTER(ctypes.c_uint8)]),
+        "rt2_tracer_query": (i32, [vp]),
+        "rt2_host_alloc": (i32, [ctypes.c_size_t, ctypes.POINTER(vp)]),
+        "rt2_host_free": (None, [vp]),
         "rt2_tracer_last_launch": (i32, [vp, ctypes.POINTER(i32), ctypes.POINTER(i32), ctypes.POINTER(i32)]),
         "rt2_tracer_on_resize": (i32, [vp, i32, i32]),
         "rt2_tracer_reset": (i32, [vp]),

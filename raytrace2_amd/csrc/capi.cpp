@@ -65,7 +65,9 @@ struct rt2_tracer {
   uint32_t* d_work = nullptr;
   unsigned long long* d_stats = nullptr;
   bool stats_on = false;
-  int64_t frame_idx = 0;
+  int64_t frame_idx = 0;  // frames launched (FrameIdx() = frame_idx + queued)
+  int queued = 0;         // Update()/Render() frames not launched yet (lazy, see rt2_tracer_render)
+  int lazy_max = 4096;    // launch once this many frames are queued (0: launch at every call)
   int max_depth = 50;
   uint64_t seed = 0x5EED2024ull;
   int launch_frames = 0;
@@ -77,6 +79,8 @@ struct rt2_tracer {
   int work_split = 64;                     // target work items per resident lane (0: one chunk)
   int batch_max = 64;                      // most work items a wave reserves with one atomic
   int last_chunk_frames = 0;
+  int occ_key = -1, occ_blocks = 1;  // cached occupancy of the last kernel instantiation
+  size_t occ_lds = 0;
   int last_variant = -1;
   int last_grid = 0;
   uint64_t launches = 0;
@@ -137,6 +141,7 @@ int Realloc(rt2_tracer* t) {
 int ResetFrame(rt2_tracer* t) {
   size_t n = (size_t)t->width * (size_t)t->local_rows;
   t->frame_idx = 0;
+  t->queued = 0;  // queued frames would only be accumulated and zeroed again
   if (n == 0) return RT2_OK;
   HIP_TRY(hipMemsetAsync(t->d_accum, 0, n * 3 * sizeof(float), t->stream));
   HIP_TRY(hipMemsetAsync(t->d_pixels, 0, n * 4, t->stream));
@@ -168,7 +173,17 @@ int DrainEvents(rt2_tracer* t) {
   return RT2_OK;
 }
 
+int Flush(rt2_tracer* t);  // launches the queued frames (rt2_tracer_render)
+
+// Flush before a setting that changes how the queued frames render.
+template <typename T>
+int FlushIfChanged(rt2_tracer* t, const T& cur, const T& next) {
+  return cur == next ? RT2_OK : Flush(t);
+}
+
 int Sync(rt2_tracer* t) {
+  int rc = Flush(t);
+  if (rc != RT2_OK) return rc;
   HIP_TRY(hipSetDevice(t->device));
   HIP_TRY(hipStreamSynchronize(t->stream));
   return DrainEvents(t);
@@ -460,18 +475,24 @@ int rt2_tracer_set_max_depth(rt2_tracer* t, int d) {
   if (!t) return Fail(RT2_ERR_INVALID, "null tracer");
   // RayTracer::max_depth is a size_t (RayTracer.hpp:32); the kernel keeps it in 16 bits
   if (d > 0xFFFF) return Fail(RT2_ERR_INVALID, "max_depth must be at most 65535");
+  int rc = FlushIfChanged(t, t->max_depth, d < 0 ? 0 : d);
+  if (rc != RT2_OK) return rc;
   t->max_depth = d < 0 ? 0 : d;
   return RT2_OK;
 }
 
 int rt2_tracer_set_samples_per_pixel(rt2_tracer* t, int spp) {
   if (!t || spp <= 0) return Fail(RT2_ERR_INVALID, "samples_per_pixel must be positive");
+  int rc = FlushIfChanged(t, t->camera.SamplesPerPixel(), spp);
+  if (rc != RT2_OK) return rc;
   t->camera.SetSamplesPerPixel(spp);
   return RT2_OK;
 }
 
 int rt2_tracer_set_seed(rt2_tracer* t, uint64_t seed) {
   if (!t) return Fail(RT2_ERR_INVALID, "null tracer");
+  int rc = FlushIfChanged(t, t->seed, seed);
+  if (rc != RT2_OK) return rc;
   t->seed = seed;
   return RT2_OK;
 }
@@ -479,6 +500,7 @@ int rt2_tracer_set_seed(rt2_tracer* t, uint64_t seed) {
 int rt2_tracer_set_partition(rt2_tracer* t, int band_h, int rank, int world) {
   if (!t || band_h < 0 || world < 1 || rank < 0 || rank >= world)
     return Fail(RT2_ERR_INVALID, "bad partition (need band_h >= 0, 0 <= rank < world)");
+  t->queued = 0;  // the partition change resets the frame
   int rc = Sync(t);
   if (rc != RT2_OK) return rc;
   t->band_h = band_h;
@@ -523,6 +545,7 @@ int rt2_tracer_last_launch(const rt2_tracer* t, int* grid, int* chunk_frames, in
 int rt2_tracer_on_resize(rt2_tracer* t, int w, int h) {
   if (!t || w <= 0 || h <= 0) return Fail(RT2_ERR_INVALID, "dims must be positive");
   if (w > 65535 || h > 65535) return Fail(RT2_ERR_INVALID, "dims must be at most 65535");
+  t->queued = 0;  // OnResize resets the frame
   int rc = Sync(t);
   if (rc != RT2_OK) return rc;
   t->width = w;
@@ -538,13 +561,15 @@ int rt2_tracer_reset(rt2_tracer* t) {
   return ResetFrame(t);
 }
 
-int rt2_tracer_render(rt2_tracer* t, int n_frames) {
-  if (!t || n_frames < 0) return Fail(RT2_ERR_INVALID, "n_frames must be >= 0");
+}  // extern "C"
+
+namespace {
+// Launches frames [frame_idx, frame_idx + n_frames) now.
+int LaunchFrames(rt2_tracer* t, int n_frames) {
   if (n_frames == 0 || t->local_rows == 0) {
     t->frame_idx += n_frames;
     return RT2_OK;
   }
-  if ((int64_t)t->frame_idx + n_frames > 0x7FFFFFFF) return Fail(RT2_ERR_INVALID, "frame index overflow");
   HIP_TRY(hipSetDevice(t->device));
   RenderParams p;
   memset(&p, 0, sizeof(p));
@@ -583,14 +608,24 @@ int rt2_tracer_render(rt2_tracer* t, int n_frames) {
   // per-record counters and per-pixel ray counts come from the counting kernel instantiation (same
   // arithmetic, extra counters); the product kernel keeps only the wave ray totals
   const bool counting = t->stats_on || t->ray_counts_on;
-  const int64_t resident = (int64_t)t->cus * RenderBlocksPerCU(variant, RenderMode(p), counting,
-                                                                 RenderLdsBytes(p)) * RenderBlockSize();
+  // resident lanes of this kernel instantiation (occupancy query cached: it costs far more than
+  // a one-frame launch)
+  const size_t lds_bytes = RenderLdsBytes(p);
+  const int okey = variant * 16 + RenderMode(p) * 2 + (counting ? 1 : 0);
+  if (t->occ_key != okey || t->occ_lds != lds_bytes) {
+    t->occ_blocks = RenderBlocksPerCU(variant, RenderMode(p), counting, lds_bytes);
+    t->occ_key = okey;
+    t->occ_lds = lds_bytes;
+  }
+  const int64_t resident = (int64_t)t->cus * t->occ_blocks * RenderBlockSize();
   // frames per launch: the caller's launch_frames, bounded by the sample-buffer budget
   const size_t frame_bytes = (size_t)p.local_pixels * 3 * sizeof(float);
   int per_launch = t->launch_frames > 0 ? std::min(t->launch_frames, n_frames) : n_frames;
   per_launch = (int)std::max<size_t>(1, std::min<size_t>((size_t)per_launch, t->sample_budget / frame_bytes));
-  const size_t need = (size_t)per_launch * frame_bytes;
+  size_t need = (size_t)per_launch * frame_bytes;
   if (need > t->samples_bytes) {
+    // grow geometrically (progressive loops raise their frames per call a little at a time)
+    need = std::max(need, std::min(2 * t->samples_bytes, (t->sample_budget / frame_bytes) * frame_bytes));
     HIP_TRY(hipStreamSynchronize(t->stream));  // the old buffer may still be read
     (void)hipFree(t->d_samples);
     t->d_samples = nullptr;
@@ -638,6 +673,40 @@ int rt2_tracer_render(rt2_tracer* t, int n_frames) {
   return RT2_OK;
 }
 
+int Flush(rt2_tracer* t) {
+  if (t->queued == 0) return RT2_OK;
+  const int n = t->queued;
+  t->queued = 0;
+  return LaunchFrames(t, n);
+}
+
+}  // namespace
+
+extern "C" {
+
+// Update()/Render() only queue frames: the queued frames are launched together when a result is
+// read (any readback, query, synchronize, stats), when a setting that affects them changes, or
+// when lazy_max frames are queued. Results cannot tell the difference (samples are summed in frame
+// order), but App::Run's headless pattern — num_samples x Update() then one readback
+// (App.cpp:243-248) — then runs as one launch instead of num_samples one-frame launches, each
+// of which would be as long as its longest path.
+int rt2_tracer_render(rt2_tracer* t, int n_frames) {
+  if (!t || n_frames < 0) return Fail(RT2_ERR_INVALID, "n_frames must be >= 0");
+  if ((int64_t)t->frame_idx + t->queued + n_frames > 0x7FFFFFFF)
+    return Fail(RT2_ERR_INVALID, "frame index overflow");
+  if (t->camera.Params().sqrt_spp <= 0) return Fail(RT2_ERR_INVALID, "samples_per_pixel gives sqrt_spp = 0");
+  t->queued += n_frames;
+  if (t->lazy_max > 0 && t->queued < t->lazy_max) return RT2_OK;
+  return Flush(t);
+}
+
+int rt2_tracer_set_lazy_frames(rt2_tracer* t, int max_queued) {
+  if (!t || max_queued < 0) return Fail(RT2_ERR_INVALID, "max_queued must be >= 0");
+  t->lazy_max = max_queued;
+  if (max_queued == 0 || t->queued >= max_queued) return Flush(t);
+  return RT2_OK;
+}
+
 int rt2_tracer_update(rt2_tracer* t) { return rt2_tracer_render(t, 1); }
 
 int rt2_tracer_synchronize(rt2_tracer* t) {
@@ -645,7 +714,7 @@ int rt2_tracer_synchronize(rt2_tracer* t) {
   return Sync(t);
 }
 
-int64_t rt2_tracer_frame_idx(const rt2_tracer* t) { return t ? t->frame_idx : -1; }
+int64_t rt2_tracer_frame_idx(const rt2_tracer* t) { return t ? t->frame_idx + t->queued : -1; }
 
 int rt2_tracer_dims(const rt2_tracer* t, int* w, int* h) {
   if (!t) return Fail(RT2_ERR_INVALID, "null tracer");
@@ -683,8 +752,42 @@ int rt2_tracer_pixels(rt2_tracer* t, uint8_t* out) {
   return RT2_OK;
 }
 
+int rt2_tracer_pixels_async(rt2_tracer* t, uint8_t* out) {
+  if (!t || !out) return Fail(RT2_ERR_INVALID, "null argument");
+  int rc = Flush(t);
+  if (rc != RT2_OK) return rc;
+  HIP_TRY(hipSetDevice(t->device));
+  size_t n = (size_t)t->width * (size_t)t->local_rows;
+  if (n) HIP_TRY(hipMemcpyAsync(out, t->d_pixels, n * 4, hipMemcpyDeviceToHost, t->stream));
+  return RT2_OK;
+}
+
+int rt2_tracer_query(rt2_tracer* t) {
+  if (!t) return Fail(RT2_ERR_INVALID, "null tracer");
+  int rc = Flush(t);
+  if (rc != RT2_OK) return rc;
+  HIP_TRY(hipSetDevice(t->device));
+  hipError_t e = hipStreamQuery(t->stream);
+  if (e == hipSuccess) return 1;
+  if (e == hipErrorNotReady) return 0;
+  return HipFail(e, "hipStreamQuery");
+}
+
+int rt2_host_alloc(size_t bytes, void** out) {
+  if (!out) return Fail(RT2_ERR_INVALID, "null argument");
+  *out = nullptr;
+  HIP_TRY(hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault));
+  return RT2_OK;
+}
+
+void rt2_host_free(void* p) {
+  if (p) (void)hipHostFree(p);
+}
+
 int rt2_tracer_copy_accum_device(rt2_tracer* t, void* dst, void* stream) {
   if (!t || !dst) return Fail(RT2_ERR_INVALID, "null argument");
+  int rc = Flush(t);
+  if (rc != RT2_OK) return rc;
   HIP_TRY(hipSetDevice(t->device));
   hipStream_t s = stream ? (hipStream_t)stream : t->stream;
   size_t n = (size_t)t->width * (size_t)t->local_rows;
@@ -720,6 +823,8 @@ int rt2_tracer_ray_counts(rt2_tracer* t, uint32_t* out) {
 
 int rt2_tracer_enable_stats(rt2_tracer* t, int on) {
   if (!t) return Fail(RT2_ERR_INVALID, "null tracer");
+  int rc = FlushIfChanged(t, t->stats_on, on != 0);
+  if (rc != RT2_OK) return rc;
   t->stats_on = on != 0;
   return RT2_OK;
 }

@@ -271,6 +271,9 @@ class RayTracer:
     def set_launch_frames(self, n: int) -> None:
         check(lib.rt2_tracer_set_launch_frames(self._h, int(n)))
 
+    def set_lazy_frames(self, max_queued: int) -> None:
+        check(lib.rt2_tracer_set_lazy_frames(self._h, int(max_queued)))
+
     def set_work_split(self, items_per_lane: int) -> None:
         check(lib.rt2_tracer_set_work_split(self._h, int(items_per_lane)))
 

@@ -58,9 +58,15 @@ def test_update_equals_render_and_chunking(have_gpu):
     a1, r1, _, _ = gpu_render("cornell_box_volume", 40, 40, 16, 7)
     a2, r2, _, _ = gpu_render("cornell_box_volume", 40, 40, 16, 7, updates=True)
     a3, r3, _, _ = gpu_render("cornell_box_volume", 40, 40, 16, 7, launch_frames=3)
+    # every Update() launched at once (no queue), and a queue flushed every 2 frames
+    a4, r4, s4, _ = gpu_render("cornell_box_volume", 40, 40, 16, 7, updates=True, lazy=0)
+    a5, r5, s5, _ = gpu_render("cornell_box_volume", 40, 40, 16, 7, updates=True, lazy=2)
     assert np.array_equal(a1.view(np.uint32), a2.view(np.uint32))
     assert np.array_equal(a1.view(np.uint32), a3.view(np.uint32))
-    assert np.array_equal(r1, r2) and np.array_equal(r1, r3)
+    assert np.array_equal(a1.view(np.uint32), a4.view(np.uint32))
+    assert np.array_equal(a1.view(np.uint32), a5.view(np.uint32))
+    assert np.array_equal(r1, r2) and np.array_equal(r1, r3) and np.array_equal(r1, r4) and np.array_equal(r1, r5)
+    assert s4["launches"] == 7 and s5["launches"] == 4
 
 
 @pytest.mark.parametrize("name", ["cornell_box_original", "final_render_book_1"])
@@ -174,3 +180,32 @@ def test_generated_stress_scene(have_gpu, tmp_path):
     assert st["overflow"] == 0
     np.testing.assert_array_equal(rc, o_rc)
     assert np.array_equal(acc.view(np.uint32), o_acc.view(np.uint32))
+
+
+def test_progressive_loop_equals_updates(have_gpu):
+    """ProgressiveLoop (frames per tick adapted to a time budget, pinned async Pixels() readback)
+    ends bit-identical to the same number of Update() calls, and each tick's pixels are Pixels()
+    of the frames done so far."""
+    import raytrace2_amd as R
+    from conftest import scene_path
+    from raytrace2_amd.progressive import ProgressiveLoop
+    w, h, frames = 96, 64, 23
+    ref = gpu_render("cornell_box_volume", w, h, 64, frames, updates=True, counts=False)
+    sc = R.Scene(scene_path("cornell_box_volume"), R.DEFAULT_SEED)
+    tr = R.RayTracer(sc, 0)
+    tr.set_seed(R.DEFAULT_SEED)
+    tr.SetSamplesPerPixel(64)
+    tr.OnResize((w, h))
+    loop = ProgressiveLoop(tr, frames, budget_ms=0.05, first_frames=2)
+    seen = []
+
+    def on_tick(lp, px):
+        assert np.array_equal(px, tr.Pixels())
+        seen.append(lp.frames_done)
+
+    loop.run(on_tick)
+    assert seen[-1] == frames and len(seen) >= 2
+    assert np.array_equal(tr.Accumulation().view(np.uint32), ref[0].view(np.uint32))
+    assert tr.FrameIdx() == frames
+    loop.close()
+    tr.close()
