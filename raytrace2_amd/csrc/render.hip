@@ -65,6 +65,15 @@ constexpr int kBlock = 256;
 #ifndef RT2_EXP_STAMPS
 #define RT2_EXP_STAMPS 0  // diagnostic build: per-section s_memtime sums into the stamp slots
 #endif
+#ifndef RT2_RARE_MIN
+#define RT2_RARE_MIN 0  // stack traversal: lanes needed before a rare, expensive step kind runs (0: off)
+#endif
+#ifndef RT2_MIN_WAVES_VOL
+#define RT2_MIN_WAVES_VOL 6
+#endif
+#ifndef RT2_MIN_WAVES_ALL
+#define RT2_MIN_WAVES_ALL 5
+#endif
 #ifndef RT2_MIN_WAVES_PER_EU
 #define RT2_MIN_WAVES_PER_EU 0  // 0: per-variant occupancy targets (kMinWaves below)
 #endif
@@ -646,6 +655,16 @@ __device__ __forceinline__ bool trace_stack(const RenderParams& P, const Nodes<k
   uint32_t acc_best = kRefNone;  // accelerated list: record of its current closest child
   while (cur != kRefNone) {
     uint32_t kind = cur >> 28, off = cur & kOffsetMask;
+    if constexpr (RT2_RARE_MIN > 0 && (Has<F, kFeatMedium>() || Has<F, kFeatXform>())) {
+      // Under divergence a branch costs the whole wave whenever one lane takes it: a lane whose
+      // next step is an expensive, infrequent kind (medium, transform entry, accelerated list)
+      // waits until RT2_RARE_MIN lanes are at such steps or no lane has other work, so those
+      // branches run for many lanes at once instead of on almost every trip. Its own step order
+      // is unchanged.
+      const bool rare = kind == kMedium || kind == kXform || kind == kListAcc;
+      const unsigned long long rm = __ballot(rare), cm = __ballot(!rare);
+      if (rare && cm != 0ull && __popcll(rm) < RT2_RARE_MIN) continue;
+    }
     if (kind == kQuad || (Has<F, kFeatSphere>() && kind == kSphere)) {
       float t;
       if (prim_t<F>(N, cur, o, d, time, tmin, tmax, t, cnt)) {
@@ -1096,9 +1115,10 @@ __device__ __forceinline__ uint32_t local_index(const RenderParams& P, uint32_t 
 template <uint32_t F, int kMode, bool kStats>
 constexpr int MinWaves() {
   if (RT2_MIN_WAVES_PER_EU > 0) return RT2_MIN_WAVES_PER_EU;
+  if (F == kFeatAll && !kStats && kMode == kModeStackGlobal) return RT2_MIN_WAVES_ALL;  // book 2
   if (kStats || kMode != kModeLinear) return 1;
   if (F == kFeatXform) return 7;                  // Cornell: 72 VGPRs
-  if (F == (kFeatXform | kFeatMedium)) return 5;  // Cornell volume: 95 VGPRs
+  if (F == (kFeatXform | kFeatMedium)) return RT2_MIN_WAVES_VOL;  // Cornell volume: 89 VGPRs at 5
   if (F == kFeatAll) return 1;
   return 6;                                       // book 1
 }
