@@ -123,6 +123,7 @@ def main():
     def step():
         tr.Reset()
         tr.Render(a.spp)
+        tr.flush()  # launch now: Render() only queues frames until a readback (rt2.h)
         if gath is not None:
             if host_gather:
                 gath.local_view().copy_(torch.from_numpy(tr.Accumulation()))

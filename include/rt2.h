@@ -114,6 +114,7 @@ RT2_API int rt2_tracer_set_launch_frames(rt2_tracer* tr, int frames_per_launch);
  * the launch, so results do not depend on the split. The buffer is bounded by `bytes` (default
  * 16 GiB): a render needing more runs as several launches. */
 RT2_API int rt2_tracer_set_lazy_frames(rt2_tracer* tr, int max_queued);
+RT2_API int rt2_tracer_flush(rt2_tracer* tr); /* launch the queued frames now (does not wait) */
 RT2_API int rt2_tracer_set_work_split(rt2_tracer* tr, int items_per_lane);
 RT2_API int rt2_tracer_set_sample_budget(rt2_tracer* tr, uint64_t bytes);
 /* Most work items a GPU wave reserves with one atomic (default 64); batches shrink as the launch

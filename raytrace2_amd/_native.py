@@ -107,6 +107,7 @@ def _load():
         "rt2_tracer_set_partition": (i32, [vp, i32, i32, i32]),
         "rt2_tracer_set_launch_frames": (i32, [vp, i32]),
         "rt2_tracer_set_lazy_frames": (i32, [vp, i32]),
+        "rt2_tracer_flush": (i32, [vp]),
         "rt2_tracer_set_work_split": (i32, [vp, i32]),
         "rt2_tracer_set_sample_budget": (i32, [vp, u64]),
         "rt2_tracer_set_batch_max": (i32, [vp, i32]),

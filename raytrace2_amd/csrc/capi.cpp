@@ -709,6 +709,11 @@ int rt2_tracer_set_lazy_frames(rt2_tracer* t, int max_queued) {
 
 int rt2_tracer_update(rt2_tracer* t) { return rt2_tracer_render(t, 1); }
 
+int rt2_tracer_flush(rt2_tracer* t) {
+  if (!t) return Fail(RT2_ERR_INVALID, "null tracer");
+  return Flush(t);
+}
+
 int rt2_tracer_synchronize(rt2_tracer* t) {
   if (!t) return Fail(RT2_ERR_INVALID, "null tracer");
   return Sync(t);

@@ -72,7 +72,7 @@ constexpr int kBlock = 256;
 #define RT2_MIN_WAVES_VOL 6
 #endif
 #ifndef RT2_MIN_WAVES_ALL
-#define RT2_MIN_WAVES_ALL 5
+#define RT2_MIN_WAVES_ALL 6
 #endif
 #ifndef RT2_MIN_WAVES_PER_EU
 #define RT2_MIN_WAVES_PER_EU 0  // 0: per-variant occupancy targets (kMinWaves below)
@@ -1115,7 +1115,8 @@ __device__ __forceinline__ uint32_t local_index(const RenderParams& P, uint32_t 
 template <uint32_t F, int kMode, bool kStats>
 constexpr int MinWaves() {
   if (RT2_MIN_WAVES_PER_EU > 0) return RT2_MIN_WAVES_PER_EU;
-  if (F == kFeatAll && !kStats && kMode == kModeStackGlobal) return RT2_MIN_WAVES_ALL;  // book 2
+  constexpr uint32_t kBook2 = kFeatSphere | kFeatMedium | kFeatXform | kFeatNoise | kFeatSpecular;
+  if ((F == kFeatAll || F == kBook2) && !kStats && kMode == kModeStackGlobal) return RT2_MIN_WAVES_ALL;  // book 2
   if (kStats || kMode != kModeLinear) return 1;
   if (F == kFeatXform) return 7;                  // Cornell: 72 VGPRs
   if (F == (kFeatXform | kFeatMedium)) return RT2_MIN_WAVES_VOL;  // Cornell volume: 89 VGPRs at 5
@@ -1461,7 +1462,8 @@ constexpr uint32_t kVariants[] = {
     kFeatXform,                                   // Cornell box
     kFeatXform | kFeatMedium,                     // Cornell volume
     kFeatSphere | kFeatSpecular | kFeatDefocus,   // RTIOW book 1
-    kFeatAll,                                     // everything (book 2, scene graphs, textures)
+    kFeatSphere | kFeatMedium | kFeatXform | kFeatNoise | kFeatSpecular,  // RTNW book 2
+    kFeatAll,                                     // everything (scene graphs, checker textures)
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
@@ -1488,6 +1490,7 @@ KernelFn Kernel(int v, int mode, bool stats) {
     case 1: return PickMode<1>(mode, stats);
     case 2: return PickMode<2>(mode, stats);
     case 3: return PickMode<3>(mode, stats);
+    case 4: return PickMode<4>(mode, stats);
   }
   return nullptr;
 }

@@ -271,6 +271,10 @@ class RayTracer:
     def set_launch_frames(self, n: int) -> None:
         check(lib.rt2_tracer_set_launch_frames(self._h, int(n)))
 
+    def flush(self) -> None:
+        """Launch the queued Update()/Render() frames now (does not wait for them)."""
+        check(lib.rt2_tracer_flush(self._h))
+
     def set_lazy_frames(self, max_queued: int) -> None:
         check(lib.rt2_tracer_set_lazy_frames(self._h, int(max_queued)))
 
