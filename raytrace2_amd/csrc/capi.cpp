@@ -52,7 +52,14 @@ struct rt2_tracer {
   uint32_t features = 0;
   int max_stack = 1;
   bool use_lds = true;
+  bool use_hybrid = true;   // stage only the BVH prefix in LDS when the scene is too large
+  bool force_hybrid = false;  // tests: hybrid even when the whole scene would fit
+  uint32_t hot_records = 0;
   int cus = 0;
+  int lds_per_cu = 0;       // bytes of LDS per CU
+  int hybrid_cap = -1;      // tests: most BVH records staged by the hybrid mode (-1: no cap)
+  int hyb_key = -1;         // cached hybrid prefix for (variant, counting)
+  uint32_t hyb_records = 0;
   float background[3] = {0, 0, 0};
   Camera camera;  // RayTracer::camera (a copy of the scene camera)
   // frame buffers (local rows)
@@ -420,13 +427,18 @@ int rt2_tracer_create(const rt2_scene* s, int device, rt2_tracer** out) {
   HIP_TRY(hipMemset(t->d_stats, 0, kStatsSlots * sizeof(unsigned long long)));
   t->root = c.root;
   t->node_records = (uint32_t)(c.nodes.size() / 4);
+  t->hot_records = c.hot_records;
   t->features = c.features;
   t->max_stack = c.max_stack;
   Put3(t->background, s->scene.background);
   t->camera = s->scene.cam;
   HIP_TRY(hipDeviceGetAttribute(&t->cus, hipDeviceAttributeMultiprocessorCount, device));
+  HIP_TRY(hipDeviceGetAttribute(&t->lds_per_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, device));
   if (const char* e = getenv("RT2_NO_LDS")) t->use_lds = e[0] == '0';
   if (const char* e = getenv("RT2_NO_LINEAR")) t->use_linear = e[0] == '0';
+  if (const char* e = getenv("RT2_NO_HYBRID")) t->use_hybrid = e[0] == '0';
+  if (const char* e = getenv("RT2_FORCE_HYBRID")) t->force_hybrid = e[0] == '1';
+  if (const char* e = getenv("RT2_HYBRID_RECORDS")) t->hybrid_cap = atoi(e);
   // App.cpp:122-125,157: scene dims when present, else the window default 1600x900
   int w = s->scene.dims_x > 0 && s->scene.dims_y > 0 ? s->scene.dims_x : 1600;
   int h = s->scene.dims_x > 0 && s->scene.dims_y > 0 ? s->scene.dims_y : 900;
@@ -598,8 +610,6 @@ int LaunchFrames(rt2_tracer* t, int n_frames) {
   p.work_counter = t->d_work;
   p.stats = t->d_stats;
   p.stack_depth = t->max_stack;
-  bool lds = t->use_lds && (size_t)t->node_records * 16 <= (size_t)kLdsSceneBytesMax;
-  p.lds_nodes = lds ? t->node_records : 0u;
   p.lin = t->d_lin;
   p.lind = t->d_lind;
   p.lin_len = t->use_linear ? t->lin_len : 0u;
@@ -608,6 +618,32 @@ int LaunchFrames(rt2_tracer* t, int n_frames) {
   // per-record counters and per-pixel ray counts come from the counting kernel instantiation (same
   // arithmetic, extra counters); the product kernel keeps only the wave ray totals
   const bool counting = t->stats_on || t->ray_counts_on;
+  // Scene records in LDS: the whole scene when it fits; otherwise (stack traversal) the top levels
+  // of the BVH — its node records are a breadth-first prefix of the record array — as many as fit
+  // beside the traversal stack without lowering the occupancy the registers allow.
+  const bool lds = t->use_lds && !t->force_hybrid && (size_t)t->node_records * 16 <= (size_t)kLdsSceneBytesMax;
+  // Measured: +20% on a 10^5-sphere field, but -15% on book 2, whose all-features kernel already
+  // spills at its occupancy target; the hybrid prefix is used for variants without media and
+  // transforms unless forced (RT2_FORCE_HYBRID).
+  const bool hybrid_variant = t->force_hybrid || !(RenderVariantFeatures(variant) & (kFeatMedium | kFeatXform));
+  uint32_t hot = 0;
+  if (!lds && hybrid_variant && t->use_lds && t->use_hybrid && t->hot_records > 0 && !p.lin_len) {
+    const int hkey = variant * 2 + (counting ? 1 : 0);
+    if (t->hyb_key != hkey) {
+      const size_t stack_bytes = (size_t)p.stack_depth * (size_t)RenderBlockSize() * 4;
+      const int blocks = RenderBlocksPerCU(variant, kModeStackHybrid, counting, stack_bytes);
+      const size_t per_block = (size_t)t->lds_per_cu / (size_t)std::max(1, blocks);
+      size_t room = per_block > stack_bytes ? (per_block - stack_bytes) / 16 : 0;
+      room = std::min(room, (size_t)kLdsHotBytesMax / 16);
+      t->hyb_records = (uint32_t)std::min<size_t>(room, t->hot_records) & ~1u;  // whole BVH records
+      t->hyb_key = hkey;
+    }
+    hot = t->hyb_records;
+    if (t->hybrid_cap >= 0) hot = std::min(hot, (uint32_t)t->hybrid_cap & ~1u);
+    if (hot < 2) hot = 0;
+  }
+  p.lds_nodes = lds ? t->node_records : hot;
+  p.lds_partial = (!lds && hot) ? 1u : 0u;
   // resident lanes of this kernel instantiation (occupancy query cached: it costs far more than
   // a one-frame launch)
   const size_t lds_bytes = RenderLdsBytes(p);

@@ -6,6 +6,7 @@
 #include <cstring>
 #include <functional>
 #include <unordered_map>
+#include <unordered_set>
 
 #include "scene.h"
 
@@ -24,6 +25,10 @@ struct Flattener {
 
   Flattener(const Scene& sc, CompiledScene& o) : s(sc), out(o) {}
 
+  // BVH node records go to the prefix [0, out.hot_records), in breadth-first order, when it is
+  // reserved (bvh_rank: BVH object -> breadth-first rank)
+  const std::unordered_map<int, uint32_t>* bvh_rank = nullptr;
+  uint32_t hot_next = 0;
   uint32_t Alloc(int records) {
     uint32_t off = (uint32_t)(out.nodes.size() / 4);
     out.nodes.resize(out.nodes.size() + 4 * (size_t)records, 0.0f);
@@ -260,7 +265,13 @@ struct Flattener {
           r = Emit(o.right, parent_xf, err);
           if (r == kRefNone) return kRefNone;
         }
-        uint32_t off = Alloc(kBvhRecords);
+        uint32_t off;
+        if (bvh_rank) {
+          off = bvh_rank->at(i) * (uint32_t)kBvhRecords;
+          hot_next += (uint32_t)kBvhRecords;
+        } else {
+          off = Alloc(kBvhRecords);
+        }
         const AABB& bb = o.aabb;
         Put(off, bb.x.min, bb.y.min, bb.z.min, Bits(l));
         Put(off + 1, bb.x.max, bb.y.max, bb.z.max, Bits(r));
@@ -455,10 +466,42 @@ bool CompileScene(const Scene& s, CompiledScene& out, std::string& err, bool acc
     err = "scene has no BVH root";
     return false;
   }
+  // BVH node records come first, in breadth-first order from the root, so any prefix of the record
+  // array holds the top levels of the tree (the stack traversal stages such a prefix in LDS when
+  // the whole scene does not fit, kModeStackHybrid); everything else follows. Record contents are
+  // the same in any order.
+  std::unordered_map<int, uint32_t> rank;
+  {
+    std::vector<int> q{s.root};
+    std::unordered_set<int> seen{s.root};
+    auto push = [&](int c) {
+      if (c >= 0 && seen.insert(c).second) q.push_back(c);
+    };
+    for (size_t h = 0; h < q.size(); h++) {
+      const Obj& o = s.objs[(size_t)q[h]];
+      if (o.kind == kBvh) {
+        rank.emplace(q[h], (uint32_t)rank.size());
+        push(o.left);
+        push(o.right);
+      } else if (o.kind == kList) {
+        for (int c : o.children) push(c);
+      } else if (o.kind == kXform || o.kind == kMedium) {
+        push(o.child);
+      }
+    }
+  }
+  const uint32_t hot = (uint32_t)rank.size() * (uint32_t)kBvhRecords;
+  out.hot_records = hot;
+  out.nodes.assign(4 * (size_t)hot, 0.0f);
   Flattener fl(s, out);
   fl.accelerate_lists = accelerate_lists;
+  fl.bvh_rank = &rank;
   out.root = fl.Emit(s.root, kRefNone, err);
   if (out.root == kRefNone) return false;
+  if (fl.hot_next != hot) {
+    err = "internal: BVH record count changed between passes";
+    return false;
+  }
   int depth = 0;
   out.max_stack = std::max(1, fl.StackNeed(s.root, depth));
   out.bvh_depth = depth;

@@ -147,9 +147,12 @@ __device__ __forceinline__ uint32_t ldg1(const uint32_t* __restrict__ p, uint32_
 template <int kMode>
 struct Nodes {
   const float4* g;
+  uint32_t lds_n;  // kModeStackHybrid: records [0, lds_n) are in LDS
   __device__ __forceinline__ float4 operator[](uint32_t i) const {
     if constexpr (kMode == kModeStackLds) {
       return s_dyn[i];
+    } else if constexpr (kMode == kModeStackHybrid) {
+      return i < lds_n ? s_dyn[i] : ldg4(g, i);
     } else {
       return ldg4(g, i);
     }
@@ -157,6 +160,12 @@ struct Nodes {
   __device__ __forceinline__ uint32_t word(uint32_t rec, uint32_t k) const {  // 32-bit word k after record rec
     if constexpr (kMode == kModeStackLds) {
       return bits(reinterpret_cast<const float*>(s_dyn + rec)[k]);
+    } else if constexpr (kMode == kModeStackHybrid) {
+      // k may run past record rec (list children, the leaf-list cursor's word(0, k)): the record
+      // that holds the word decides where it lives
+      const uint32_t w = 4u * rec + k;
+      return (w >> 2) < lds_n ? bits(reinterpret_cast<const float*>(s_dyn)[w])
+                              : ldg1(reinterpret_cast<const uint32_t*>(g), w);
     } else {
       return ldg1(reinterpret_cast<const uint32_t*>(g + rec), k);
     }
@@ -1109,14 +1118,16 @@ __device__ __forceinline__ uint32_t local_index(const RenderParams& P, uint32_t 
   return r * (uint32_t)P.width + x;
 }
 
-// Occupancy target (waves per SIMD the register allocation must allow) for the threaded-traversal
-// product kernels: the highest that compiles without VGPR spills. Stack-traversal and stats
-// kernels keep the compiler's own allocation (their LDS stack bounds occupancy anyway).
+// Occupancy target (waves per SIMD the register allocation must allow), chosen per variant by
+// measurement: Cornell 7 (no spills), Cornell volume 6 and the book 2 / all-features stack kernels
+// 6 (some spills, faster than fewer waves: their loads are latency bound), book 1 6. Other stack
+// and the counting kernels keep the compiler's own allocation.
 template <uint32_t F, int kMode, bool kStats>
 constexpr int MinWaves() {
   if (RT2_MIN_WAVES_PER_EU > 0) return RT2_MIN_WAVES_PER_EU;
   constexpr uint32_t kBook2 = kFeatSphere | kFeatMedium | kFeatXform | kFeatNoise | kFeatSpecular;
-  if ((F == kFeatAll || F == kBook2) && !kStats && kMode == kModeStackGlobal) return RT2_MIN_WAVES_ALL;  // book 2
+  if ((F == kFeatAll || F == kBook2) && !kStats && (kMode == kModeStackGlobal || kMode == kModeStackHybrid))
+    return RT2_MIN_WAVES_ALL;  // book 2
   if (kStats || kMode != kModeLinear) return 1;
   if (F == kFeatXform) return 7;                  // Cornell: 72 VGPRs
   if (F == (kFeatXform | kFeatMedium)) return RT2_MIN_WAVES_VOL;  // Cornell volume: 89 VGPRs at 5
@@ -1126,13 +1137,14 @@ constexpr int MinWaves() {
 
 template <uint32_t F, int kMode, bool kStats>
 __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render_kernel(const RenderParams P) {
-  Nodes<kMode> N{reinterpret_cast<const float4*>(P.nodes)};
-  if constexpr (kMode == kModeStackLds) {
+  constexpr bool kLds = kMode == kModeStackLds || kMode == kModeStackHybrid;
+  Nodes<kMode> N{reinterpret_cast<const float4*>(P.nodes), P.lds_nodes};
+  if constexpr (kLds) {
     const float4* src = reinterpret_cast<const float4*>(P.nodes);
     for (uint32_t i = threadIdx.x; i < P.lds_nodes; i += kBlock) s_dyn[i] = src[i];
     __syncthreads();
   }
-  uint32_t* stk = reinterpret_cast<uint32_t*>(s_dyn + (kMode == kModeStackLds ? P.lds_nodes : 0u)) + threadIdx.x;
+  uint32_t* stk = reinterpret_cast<uint32_t*>(s_dyn + (kLds ? P.lds_nodes : 0u)) + threadIdx.x;
   const int lane = (int)__lane_id();
   const float4* M = reinterpret_cast<const float4*>(P.materials);
   const f3 bg = mk(P.background[0], P.background[1], P.background[2]);
@@ -1480,6 +1492,7 @@ KernelFn PickMode(int mode, bool stats) {
   switch (mode) {
     case kModeStackLds: return Pick<V, kModeStackLds>(stats);
     case kModeLinear: return Pick<V, kModeLinear>(stats);
+    case kModeStackHybrid: return Pick<V, kModeStackHybrid>(stats);
     default: return Pick<V, kModeStackGlobal>(stats);
   }
 }
@@ -1561,7 +1574,8 @@ uint32_t RenderVariantFeatures(int v) { return dev::kVariants[v]; }
 
 int RenderMode(const RenderParams& p) {
   if (p.lin_len) return kModeLinear;
-  return p.lds_nodes ? kModeStackLds : kModeStackGlobal;
+  if (!p.lds_nodes) return kModeStackGlobal;
+  return p.lds_partial ? kModeStackHybrid : kModeStackLds;
 }
 
 size_t RenderLdsBytes(const RenderParams& p) {

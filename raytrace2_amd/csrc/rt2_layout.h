@@ -122,7 +122,10 @@ constexpr int kLinearMaxSteps = 1024;  // scenes whose program is longer use the
 constexpr uint32_t kLinearMaxRun = RT2_LINEAR_MAX_RUN;  // quads per run (3-bit axis codes in one word)
 constexpr int kLinearMaxXformDepth = 8;  // deeper transform nesting uses the stack traversal
 
-enum TraversalMode : int { kModeStackGlobal = 0, kModeStackLds = 1, kModeLinear = 2 };
+// kModeStackHybrid: the scene is too large for LDS, but its BVH node records (the prefix
+// [0, lds_nodes) of the record array) are staged in LDS; other records are read from global memory.
+enum TraversalMode : int { kModeStackGlobal = 0, kModeStackLds = 1, kModeLinear = 2, kModeStackHybrid = 3 };
+constexpr int kLdsHotBytesMax = 32 * 1024;  // BVH prefix staged in LDS by kModeStackHybrid
 
 struct CameraParams {
   float pixel00[3], du[3], dv[3], center[3], defocus_u[3], defocus_v[3];
@@ -164,6 +167,7 @@ struct RenderParams {
   unsigned long long* stats;  // StatsCounters::kCount slots
   int stack_depth;         // traversal-stack entries per lane (<= kTraversalStack)
   uint32_t lds_nodes;      // float4 records staged in LDS (0: read the scene from global memory)
+  uint32_t lds_partial;    // 1: only the BVH prefix is in LDS (kModeStackHybrid)
   const void* lin;         // uint4[lin_len] threaded traversal program (kModeLinear)
   const void* lind;        // float4 records of the program's steps (kModeLinear)
   uint32_t lin_len;

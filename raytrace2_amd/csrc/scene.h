@@ -133,7 +133,8 @@ bool LoadAppSettingsFile(const std::string& path, AppSettings& out, std::string&
 
 // Flattened scene program (rt2_layout.h) ready for upload.
 struct CompiledScene {
-  std::vector<float> nodes;  // float4 records
+  std::vector<float> nodes;  // float4 records; BVH node records first ([0, hot_records))
+  uint32_t hot_records = 0;
   uint32_t root = kRefNone;
   std::vector<float> materials;
   std::vector<float> textures;

@@ -134,15 +134,18 @@ def test_full_size_rows_subset(have_gpu):
     assert np.array_equal(acc.view(np.uint32), o_acc.view(np.uint32))
 
 
-MODES = {"linear": {}, "stack_lds": {"RT2_NO_LINEAR": "1"}, "stack_global": {"RT2_NO_LINEAR": "1", "RT2_NO_LDS": "1"}}
+MODES = {"linear": {}, "stack_lds": {"RT2_NO_LINEAR": "1"}, "stack_global": {"RT2_NO_LINEAR": "1", "RT2_NO_LDS": "1"},
+         "stack_hybrid": {"RT2_NO_LINEAR": "1", "RT2_FORCE_HYBRID": "1"},
+         "stack_hybrid_top3": {"RT2_NO_LINEAR": "1", "RT2_FORCE_HYBRID": "1", "RT2_HYBRID_RECORDS": "6"}}
 
 
 @pytest.mark.parametrize("mode", list(MODES))
 @pytest.mark.parametrize("name,w,h,spp,frames", [c for c in CASES if c[0] != "book2_final_scene_10000_samples"],
                          ids=[c[0] for c in CASES if c[0] != "book2_final_scene_10000_samples"])
 def test_every_traversal_mode_matches(have_gpu, monkeypatch, mode, name, w, h, spp, frames):
-    """The threaded lockstep traversal and the stack traversal (LDS or global scene) visit nodes in
-    the same per-lane order, so every mode is bit-identical to the oracle."""
+    """The threaded lockstep traversal and the stack traversal (scene in LDS, in global memory, or
+    only the top of its BVH in LDS) visit nodes in the same per-lane order, so every mode is
+    bit-identical to the oracle."""
     for k, v in MODES[mode].items():
         monkeypatch.setenv(k, v)
     acc, rc, st, _ = gpu_render(name, w, h, spp, min(frames, 4))
