@@ -621,24 +621,30 @@ int LaunchFrames(rt2_tracer* t, int n_frames) {
   // Scene records in LDS: the whole scene when it fits; otherwise (stack traversal) the top levels
   // of the BVH — its node records are a breadth-first prefix of the record array — as many as fit
   // beside the traversal stack without lowering the occupancy the registers allow.
-  const bool lds = t->use_lds && !t->force_hybrid && (size_t)t->node_records * 16 <= (size_t)kLdsSceneBytesMax;
-  // Measured: +20% on a 10^5-sphere field, but -15% on book 2, whose all-features kernel already
-  // spills at its occupancy target; the hybrid prefix is used for variants without media and
-  // transforms unless forced (RT2_FORCE_HYBRID).
-  const bool hybrid_variant = t->force_hybrid || !(RenderVariantFeatures(variant) & (kFeatMedium | kFeatXform));
-  uint32_t hot = 0;
-  if (!lds && hybrid_variant && t->use_lds && t->use_hybrid && t->hot_records > 0 && !p.lin_len) {
+  // LDS room per workgroup that keeps the occupancy the registers allow (beside the stack)
+  uint32_t room = 0;  // float4 records
+  if (t->use_lds && !p.lin_len) {
     const int hkey = variant * 2 + (counting ? 1 : 0);
     if (t->hyb_key != hkey) {
       const size_t stack_bytes = (size_t)p.stack_depth * (size_t)RenderBlockSize() * 4;
       const int blocks = RenderBlocksPerCU(variant, kModeStackHybrid, counting, stack_bytes);
       const size_t per_block = (size_t)t->lds_per_cu / (size_t)std::max(1, blocks);
-      size_t room = per_block > stack_bytes ? (per_block - stack_bytes) / 16 : 0;
-      room = std::min(room, (size_t)kLdsHotBytesMax / 16);
-      t->hyb_records = (uint32_t)std::min<size_t>(room, t->hot_records) & ~1u;  // whole BVH records
+      t->hyb_records = (uint32_t)(per_block > stack_bytes ? (per_block - stack_bytes) / 16 : 0);
       t->hyb_key = hkey;
     }
-    hot = t->hyb_records;
+    room = t->hyb_records;
+  }
+  // whole scene in LDS only when that costs no occupancy (measured on book 1 in stack mode: the
+  // 32 KB scene in LDS limited it to 3 workgroups per CU, 3.9 Grays/s; the hybrid prefix 5.0)
+  const bool lds = t->use_lds && !t->force_hybrid && !p.lin_len && t->node_records <= room &&
+                   (size_t)t->node_records * 16 <= (size_t)kLdsSceneBytesMax;
+  // Hybrid prefix: measured +20% on a 10^5-sphere field, but -15% on book 2, whose all-features
+  // kernel already spills at its occupancy target; used for variants without media and transforms
+  // unless forced (RT2_FORCE_HYBRID).
+  const bool hybrid_variant = t->force_hybrid || !(RenderVariantFeatures(variant) & (kFeatMedium | kFeatXform));
+  uint32_t hot = 0;
+  if (!lds && hybrid_variant && t->use_lds && t->use_hybrid && t->hot_records > 0 && !p.lin_len) {
+    hot = std::min<uint32_t>(std::min<uint32_t>(room, (uint32_t)(kLdsHotBytesMax / 16)), t->hot_records) & ~1u;
     if (t->hybrid_cap >= 0) hot = std::min(hot, (uint32_t)t->hybrid_cap & ~1u);
     if (hot < 2) hot = 0;
   }
