@@ -1,0 +1,53 @@
+"""C-ABI error behaviour and host-side bookkeeping of a live tracer (needs the GPU): invalid
+arguments return RT2_ERR_INVALID with a message and leave the tracer usable; FrameIdx counts queued
+frames; Reset drops them."""
+import numpy as np
+import pytest
+
+import raytrace2_amd as R
+from conftest import scene_path
+from raytrace2_amd._native import Rt2Error
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def tracer(have_gpu):
+    sc = R.Scene(scene_path("cornell_box_original"), R.DEFAULT_SEED)
+    tr = R.RayTracer(sc, 0)
+    tr.SetSamplesPerPixel(16)
+    tr.OnResize((24, 16))
+    yield tr
+    tr.close()
+
+
+@pytest.mark.parametrize("call", [
+    lambda tr: setattr(tr, "max_depth", 70000),
+    lambda tr: tr.OnResize((0, 5)),
+    lambda tr: tr.OnResize((70000, 5)),
+    lambda tr: tr.Render(-1),
+    lambda tr: tr.SetSamplesPerPixel(0),
+    lambda tr: tr.set_work_split(-1),
+    lambda tr: tr.set_batch_max(0),
+    lambda tr: tr.set_lazy_frames(-1),
+    lambda tr: tr.set_partition(8, 3, 2),
+])
+def test_invalid_arguments_fail_loudly_and_keep_the_tracer(tracer, call):
+    with pytest.raises(Rt2Error) as e:
+        call(tracer)
+    assert e.value.args and "rt2 error -1" in str(e.value)
+    tracer.Render(2)
+    assert tracer.FrameIdx() == 2 and np.isfinite(tracer.NonConvertedPixels()).all()
+
+
+def test_queued_frames_and_reset(tracer):
+    for _ in range(5):
+        tracer.Update()
+    assert tracer.FrameIdx() == 5 and tracer.stats()["launches"] == 1  # stats() launched the queue
+    tracer.Update()
+    tracer.Reset()  # drops the queued frame: nothing is launched for it
+    assert tracer.FrameIdx() == 0 and tracer.stats()["launches"] == 1
+    assert not tracer.Accumulation().any()
+    tracer.Render(3)
+    a = tracer.Accumulation()
+    assert tracer.FrameIdx() == 3 and a.any()

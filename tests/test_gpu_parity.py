@@ -212,3 +212,15 @@ def test_progressive_loop_equals_updates(have_gpu):
     assert tr.FrameIdx() == frames
     loop.close()
     tr.close()
+
+
+@pytest.mark.parametrize("w,h", [(1, 1), (1, 7), (13, 1), (9, 9), (65, 3)])
+def test_ragged_and_tiny_images(have_gpu, w, h):
+    """Images smaller than one 8x8 tile or with partial edge tiles: edge lanes get no pixel, every
+    real pixel is rendered once per frame, bit-identical to the oracle."""
+    acc, rc, st, px = gpu_render("cornell_box_original", w, h, 16, 5)
+    o_acc, o_rc, o_cnt = oracle_render("cornell_box_original", w, h, 16, 5, forward=True)
+    assert acc.shape == (h, w, 3) and px.shape == (h, w, 4)
+    np.testing.assert_array_equal(rc, o_rc)
+    assert st["rays"] == o_cnt["rays"] and st["paths"] == w * h * 5
+    assert np.array_equal(acc.view(np.uint32), o_acc.view(np.uint32))
