@@ -44,6 +44,7 @@ struct rt2_tracer {
   void* d_perlin_vec = nullptr;
   int* d_perlin_perm = nullptr;
   void* d_lin = nullptr;
+  void* d_lin_wide = nullptr;
   void* d_lind = nullptr;
   uint32_t lin_len = 0;
   bool use_linear = true;
@@ -419,6 +420,7 @@ int rt2_tracer_create(const rt2_scene* s, int device, rt2_tracer** out) {
   if ((rc = Upload(&t->d_perlin_perm, c.perlin_perm.data(), c.perlin_perm.size() * sizeof(int))) != RT2_OK) return rc;
   if (!c.lin.empty()) {
     if ((rc = Upload(&t->d_lin, c.lin.data(), c.lin.size() * sizeof(uint32_t))) != RT2_OK) return rc;
+    if ((rc = Upload(&t->d_lin_wide, c.lin_wide.data(), c.lin_wide.size() * sizeof(uint32_t))) != RT2_OK) return rc;
     if ((rc = Upload(&t->d_lind, c.lind.data(), c.lind.size() * sizeof(float))) != RT2_OK) return rc;
     t->lin_len = (uint32_t)(c.lin.size() / 4);
   }
@@ -468,6 +470,7 @@ void rt2_tracer_destroy(rt2_tracer* t) {
   (void)hipFree(t->d_perlin_vec);
   (void)hipFree(t->d_perlin_perm);
   (void)hipFree(t->d_lin);
+  (void)hipFree(t->d_lin_wide);
   (void)hipFree(t->d_lind);
   (void)hipFree(t->d_work);
   (void)hipFree(t->d_stats);
@@ -611,6 +614,7 @@ int LaunchFrames(rt2_tracer* t, int n_frames) {
   p.stats = t->d_stats;
   p.stack_depth = t->max_stack;
   p.lin = t->d_lin;
+  p.lin_wide = t->d_lin_wide;
   p.lind = t->d_lind;
   p.lin_len = t->use_linear ? t->lin_len : 0u;
   uint32_t feats = t->features | (p.cam.defocus_angle > 0.0f ? (uint32_t)kFeatDefocus : 0u);

@@ -540,6 +540,17 @@ bool CompileScene(const Scene& s, CompiledScene& out, std::string& err, bool acc
       out.lin[4 * i + 1] = codes;
     }
   }
+  // Wide program: each 16-byte step entry followed by the first 48 bytes of its record (a whole BVH
+  // node or QUADAA quad), so one 64-byte scalar load fetches both
+  {
+    size_t n = out.lin.size() / 4;
+    out.lin_wide.assign(16 * n, 0u);
+    for (size_t i = 0; i < n; i++) {
+      for (int k = 0; k < 4; k++) out.lin_wide[16 * i + k] = out.lin[4 * i + k];
+      const size_t rec = 4 * (size_t)out.lin[4 * i + 2];
+      for (size_t k = 0; k < 12 && rec + k < out.lind.size(); k++) memcpy(&out.lin_wide[16 * i + 4 + k], &out.lind[rec + k], 4);
+    }
+  }
   PackMaterials(s, out);
   PackTextures(s, out);
   if (out.spheres) out.features |= kFeatSphere;

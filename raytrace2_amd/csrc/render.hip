@@ -65,6 +65,9 @@ constexpr int kBlock = 256;
 #ifndef RT2_EXP_STAMPS
 #define RT2_EXP_STAMPS 0  // diagnostic build: per-section s_memtime sums into the stamp slots
 #endif
+#ifndef RT2_WIDE_PROGRAM
+#define RT2_WIDE_PROGRAM 1  // threaded program: 64-byte steps (entry + first 48 record bytes, one load)
+#endif
 #ifndef RT2_RARE_MIN
 #define RT2_RARE_MIN 0  // stack traversal: lanes needed before a rare, expensive step kind runs (0: off)
 #endif
@@ -810,7 +813,9 @@ template <uint32_t F, bool kStats>
 __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd, float time, Path& path, HitRef& h,
                                              Counters& cnt) {
   const Nodes<kModeLinear> N{reinterpret_cast<const float4*>(P.lind)};  // boundaries / nested xforms
+#if !RT2_WIDE_PROGRAM
   const void* prog = P.lin;
+#endif
   const void* recs = P.lind;
   f3 o = wo, d = wd;
   const f3 winv = recip3(wd);
@@ -833,7 +838,12 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
     unsigned long long lower;
     while ((lower = __ballot(next < i)) != 0ull) i = __builtin_amdgcn_readlane(next, __ffsll((long long)lower) - 1);
     if (i >= len) break;
+#if RT2_WIDE_PROGRAM
+    const u32x16 sw = sld16(P.lin_wide, i * 64u);  // entry + the first 48 bytes of its record
+    const u32x4 st = {sw[0], sw[1], sw[2], sw[3]};
+#else
     const u32x4 st = sld4(prog, i * 16u);
+#endif
     const uint32_t kind = st.x, off = st.z;
     RT2_WAVE(1);
     if (kind == kBvh) RT2_WAVE(2);
@@ -851,7 +861,11 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
     next = i + 1u;
     if (kind == kBvh) {
       if (kStats) cnt.bvh++;
+#if RT2_WIDE_PROGRAM
+      const u32x8 b = {sw[4], sw[5], sw[6], sw[7], sw[8], sw[9], sw[10], sw[11]};
+#else
       const u32x8 b = sld8(recs, off * 16u);
+#endif
       float4 lo = make_float4(uf(b[0]), uf(b[1]), uf(b[2]), 0.0f), hi = make_float4(uf(b[4]), uf(b[5]), uf(b[6]), 0.0f);
 #if RT2_EXP_NO_FIN_AABB
       const bool in = aabb_hit(lo, hi, o, inv, tmin, tmax);
@@ -871,7 +885,12 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
         bool ok0;
         uint32_t kind0;
         if (c0 >= 4u) {
+#if RT2_WIDE_PROGRAM
+          const u32x8 a = k == 0u ? u32x8{sw[4], sw[5], sw[6], sw[7], sw[8], sw[9], sw[10], sw[11]}
+                                  : sld8(recs, o0 * 16u);
+#else
           const u32x8 a = sld8(recs, o0 * 16u);
+#endif
           float ra[8];
 #pragma unroll
           for (int j = 0; j < 8; j++) ra[j] = uf(a[j]);

@@ -170,6 +170,7 @@ struct RenderParams {
   uint32_t lds_partial;    // 1: only the BVH prefix is in LDS (kModeStackHybrid)
   const void* lin;         // uint4[lin_len] threaded traversal program (kModeLinear)
   const void* lind;        // float4 records of the program's steps (kModeLinear)
+  const void* lin_wide;    // 64-byte steps: entry + first 48 bytes of its record (kModeLinear)
   uint32_t lin_len;
 };
 
