@@ -184,6 +184,11 @@ struct Nodes {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
+__device__ __forceinline__ uint32_t sld1(const void* base, uint32_t off) {
+  uint32_t v;
+  asm("s_load_dword %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(base), "s"(off));
+  return v;
+}
 __device__ __forceinline__ u32x4 sld4(const void* base, uint32_t off) {
   u32x4 v;
   asm("s_load_dwordx4 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(base), "s"(off));
@@ -635,6 +640,82 @@ __device__ __forceinline__ bool medium_t(const Nodes<kMode>& N, uint32_t off, f3
   return true;
 }
 
+// ConstantMedium boundary in the threaded traversal: the medium step is wave-uniform, so its
+// boundary records are scalar loads, and an axis-aligned boundary quad (every box face) takes the
+// axis-aligned test with IEEE division (quad_cand_aa, the same decision and t as Quad::Hit).
+template <uint32_t F>
+__device__ __forceinline__ bool boundary_prim_lin(const void* recs, uint32_t ref, f3 o, f3 d, float time, float lo,
+                                                  float hi, float& t_out, Counters& cnt) {
+  const uint32_t off = ref & kOffsetMask;
+  if (Has<F, kFeatSphere>() && (ref >> 28) == kSphere) {
+    cnt.sphere++;
+    return sphere_t(Nodes<kModeLinear>{reinterpret_cast<const float4*>(recs), 0u}, off, o, d, time, lo, hi, t_out);
+  }
+  cnt.quad++;
+  u32x16 a;
+  u32x4 b2;
+  sld20(recs, off * 16u, a, b2);
+  float w[20];
+#pragma unroll
+  for (int j = 0; j < 16; j++) w[j] = uf(a[j]);
+#pragma unroll
+  for (int j = 0; j < 4; j++) w[16 + j] = uf(b2[j]);
+  const uint32_t code = a[11];  // axis code (compile.cpp): k + 1, or k + 4 for a unit normal
+  float t;
+  bool ok;
+  if (code == 1u || code == 4u) {
+    ok = quad_cand_aa<0>(w, o, d, t);
+  } else if (code == 2u || code == 5u) {
+    ok = quad_cand_aa<1>(w, o, d, t);
+  } else if (code == 3u || code == 6u) {
+    ok = quad_cand_aa<2>(w, o, d, t);
+  } else {
+    ok = quad_cand_w(w, o, d, t);
+  }
+  if (!(ok && lo <= t && t <= hi)) return false;  // Quad::Hit: Contains (inclusive)
+  t_out = t;
+  return true;
+}
+
+template <uint32_t F>
+__device__ __forceinline__ bool boundary_t_lin(const void* recs, uint32_t ref, f3 o, f3 d, float time, float lo,
+                                               float hi, float& t_out, Counters& cnt) {
+  if ((ref >> 28) != kList) return boundary_prim_lin<F>(recs, ref, o, d, time, lo, hi, t_out, cnt);
+  const uint32_t off = ref & kOffsetMask;
+  const uint32_t n = sld1(recs, off * 16u);
+  bool any = false;
+  for (uint32_t k = 0; k < n; k++) {  // HittableList::Hit (HittableList.cpp:8-22)
+    float t;
+    if (boundary_prim_lin<F>(recs, sld1(recs, (off + 1u) * 16u + 4u * k), o, d, time, lo, hi, t, cnt)) {
+      any = true;
+      hi = t;
+    }
+  }
+  if (any) t_out = hi;
+  return any;
+}
+
+// medium_t with the boundary queries above (same operations, same random draw)
+template <uint32_t F>
+__device__ __forceinline__ bool medium_t_lin(const void* recs, uint32_t off, f3 o, f3 d, float time, float tmin,
+                                             float tmax, Path& path, float& t_out, Counters& cnt) {
+  const u32x4 r0 = sld4(recs, off * 16u);
+  const uint32_t bref = r0.z;
+  float t1, t2;
+  if (!boundary_t_lin<F>(recs, bref, o, d, time, -FLT_MAX, FLT_MAX, t1, cnt)) return false;
+  if (!boundary_t_lin<F>(recs, bref, o, d, time, (float)((double)t1 + 0.0001), FLT_MAX, t2, cnt)) return false;
+  t1 = fmaxf(t1, tmin);
+  t2 = fminf(t2, tmax);
+  if (t1 >= t2) return false;
+  t1 = fmaxf(t1, 0.0f);
+  float len = sqrtf(dot(d, d));
+  float inside = (t2 - t1) * len;
+  float hit_dist = uf(r0.x) * (float)log((double)path.uniform());
+  if (hit_dist > inside) return false;
+  t_out = t1 + hit_dist / len;
+  return true;
+}
+
 struct HitRef {
   float t;
   uint32_t prim;  // ref of the quad / sphere / medium that produced the closest hit
@@ -951,7 +1032,7 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
     } else if (Has<F, kFeatMedium>() && kind == kMedium) {
       if (kStats) cnt.medium++;
       float t;
-      if (medium_t<F>(N, off, o, d, time, tmin, tmax, path, t, cnt)) {
+      if (medium_t_lin<F>(recs, off, o, d, time, tmin, tmax, path, t, cnt)) {
         tmax = t;
         prim = make_ref(kMedium, off);
         h.xf = cur_xf;
