@@ -71,6 +71,9 @@ constexpr int kBlock = 256;
 #ifndef RT2_RARE_MIN
 #define RT2_RARE_MIN 0  // stack traversal: lanes needed before a rare, expensive step kind runs (0: off)
 #endif
+#ifndef RT2_MIN_WAVES_BOOK1
+#define RT2_MIN_WAVES_BOOK1 8
+#endif
 #ifndef RT2_MIN_WAVES_VOL
 #define RT2_MIN_WAVES_VOL 6
 #endif
@@ -426,10 +429,8 @@ __device__ __forceinline__ bool quad_t(const Nodes<kMode>& N, uint32_t off, f3 o
 }
 
 // Sphere::Hit (Sphere.cpp:7-37): exclusive interval (Surrounds); uv is dead output
-template <int kMode>
-__device__ __forceinline__ bool sphere_t(const Nodes<kMode>& N, uint32_t off, f3 o, f3 d, float time, float tmin,
-                                         float tmax, float& t_out) {
-  float4 r0 = N[off], r1 = N[off + 1];
+__device__ __forceinline__ bool sphere_t_rec(float4 r0, float4 r1, f3 o, f3 d, float time, float tmin, float tmax,
+                                             float& t_out) {
   f3 center = xyz(r0) + xyz(r1) * time;
   f3 oc = center - o;
   float a = dot(d, d);
@@ -445,6 +446,11 @@ __device__ __forceinline__ bool sphere_t(const Nodes<kMode>& N, uint32_t off, f3
   }
   t_out = root;
   return true;
+}
+template <int kMode>
+__device__ __forceinline__ bool sphere_t(const Nodes<kMode>& N, uint32_t off, f3 o, f3 d, float time, float tmin,
+                                         float tmax, float& t_out) {
+  return sphere_t_rec(N[off], N[off + 1], o, d, time, tmin, tmax, t_out);
 }
 
 // Quad::Hit split in two: the candidate (pure function of the ray) and the interval test. The
@@ -999,7 +1005,15 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
     } else if (Has<F, kFeatSphere>() && kind == kSphere) {
       float t;
       uint32_t ref = make_ref(kind, off);
-      if (prim_t<F>(N, ref, o, d, time, tmin, tmax, t, cnt)) {
+#if RT2_WIDE_PROGRAM
+      // the sphere record (c0, r | disp, mat) is the step's inline words: no load
+      if (kStats) cnt.sphere++;
+      const bool hs = sphere_t_rec(make_float4(uf(sw[4]), uf(sw[5]), uf(sw[6]), uf(sw[7])),
+                                   make_float4(uf(sw[8]), uf(sw[9]), uf(sw[10]), uf(sw[11])), o, d, time, tmin, tmax, t);
+#else
+      const bool hs = prim_t<F>(N, ref, o, d, time, tmin, tmax, t, cnt);
+#endif
+      if (hs) {
         tmax = t;
         prim = ref;
         h.xf = cur_xf;
@@ -1232,7 +1246,7 @@ constexpr int MinWaves() {
   if (F == kFeatXform) return 7;                  // Cornell: 72 VGPRs
   if (F == (kFeatXform | kFeatMedium)) return RT2_MIN_WAVES_VOL;  // Cornell volume: 89 VGPRs at 5
   if (F == kFeatAll) return 1;
-  return 6;                                       // book 1
+  return RT2_MIN_WAVES_BOOK1;                     // book 1
 }
 
 template <uint32_t F, int kMode, bool kStats>
