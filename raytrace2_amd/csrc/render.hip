@@ -703,9 +703,8 @@ __device__ __forceinline__ bool boundary_t_lin(const void* recs, uint32_t ref, f
 
 // medium_t with the boundary queries above (same operations, same random draw)
 template <uint32_t F>
-__device__ __forceinline__ bool medium_t_lin(const void* recs, uint32_t off, f3 o, f3 d, float time, float tmin,
+__device__ __forceinline__ bool medium_t_lin(const void* recs, const u32x4 r0, f3 o, f3 d, float time, float tmin,
                                              float tmax, Path& path, float& t_out, Counters& cnt) {
-  const u32x4 r0 = sld4(recs, off * 16u);
   const uint32_t bref = r0.z;
   float t1, t2;
   if (!boundary_t_lin<F>(recs, bref, o, d, time, -FLT_MAX, FLT_MAX, t1, cnt)) return false;
@@ -1046,7 +1045,12 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
     } else if (Has<F, kFeatMedium>() && kind == kMedium) {
       if (kStats) cnt.medium++;
       float t;
-      if (medium_t_lin<F>(recs, off, o, d, time, tmin, tmax, path, t, cnt)) {
+#if RT2_WIDE_PROGRAM
+      const u32x4 mr = {sw[4], sw[5], sw[6], sw[7]};  // the medium record, inline
+#else
+      const u32x4 mr = sld4(recs, off * 16u);
+#endif
+      if (medium_t_lin<F>(recs, mr, o, d, time, tmin, tmax, path, t, cnt)) {
         tmax = t;
         prim = make_ref(kMedium, off);
         h.xf = cur_xf;
