@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <unordered_map>
@@ -291,6 +292,14 @@ struct Flattener {
   // every visited record in program order (`lind`), so consecutive steps read consecutive bytes.
   // References inside copied records (XFORM parent, medium boundary) point into `lind`.
   // Returns false when the program would exceed kLinearMaxSteps.
+  // kLinearMaxSteps, or RT2_LINEAR_MAX_STEPS from the environment (ablation of the mode switch)
+  static size_t LinearMaxSteps() {
+    static const size_t v = [] {
+      const char* e = getenv("RT2_LINEAR_MAX_STEPS");
+      return e ? (size_t)strtoul(e, nullptr, 10) : (size_t)kLinearMaxSteps;
+    }();
+    return v;
+  }
   uint32_t CopyRecords(uint32_t src_off, int n, std::vector<float>& lind) {
     uint32_t off = (uint32_t)(lind.size() / 4);
     const float* r = out.nodes.data() + 4 * (size_t)src_off;
@@ -309,8 +318,35 @@ struct Flattener {
     for (size_t k = 0; k < kids.size(); k++) lind[4 * (off + 1 + k / 4) + k % 4] = Bits(kids[k]);
     return make_ref(kList, off);
   }
+  // An accelerated list's tree in the threaded program: ACCBVH steps (padded box, skip = index
+  // after the subtree) near child first, ACCSPHERE steps with aux = the sphere's record offset in
+  // the node array, which is the list's child order (the kernel breaks equal roots by it).
+  bool LinearizeAcc(uint32_t ref, std::vector<uint32_t>& lin, std::vector<float>& lind) {
+    if (lin.size() / 4 >= LinearMaxSteps()) return false;
+    const uint32_t kind = ref >> 28, off = ref & kOffsetMask;
+    if (kind == kAccSphere) {
+      lin.insert(lin.end(), {kAccSphere, 0u, CopyRecords(off, kSphereRecords, lind), off});
+      return true;
+    }
+    const size_t me = lin.size() / 4;
+    lin.insert(lin.end(), {kAccBvh, 0u, CopyRecords(off, kBvhRecords, lind), 0u});
+    uint32_t near_ref, far_ref;
+    memcpy(&near_ref, &out.nodes[4 * (size_t)off + 3], 4);
+    memcpy(&far_ref, &out.nodes[4 * (size_t)off + 7], 4);
+    if (!LinearizeAcc(near_ref, lin, lind) || !LinearizeAcc(far_ref, lin, lind)) return false;
+    lin[4 * me + 1] = (uint32_t)(lin.size() / 4);
+    return true;
+  }
+  bool ContainsAccList(int i) const {
+    const Obj& o = s.objs[(size_t)i];
+    if (o.kind == kList && acc_depth.count(i)) return true;
+    if (o.kind == kList)
+      for (int c : o.children)
+        if (ContainsAccList(c)) return true;
+    return false;
+  }
   bool Linearize(int i, uint32_t parent_xf, std::vector<uint32_t>& lin, std::vector<float>& lind, int xf_depth = 0) {
-    if (lin.size() / 4 >= (size_t)kLinearMaxSteps) return false;
+    if (lin.size() / 4 >= LinearMaxSteps()) return false;
     const Obj& o = s.objs[(size_t)i];
     uint32_t src = ref_of.at(i) & kOffsetMask;
     auto emit = [&](uint32_t kind, uint32_t rec, uint32_t aux) {
@@ -328,7 +364,12 @@ struct Flattener {
         return true;
       }
       case kList:
-        if (acc_depth.count(i)) return false;  // accelerated lists use the stack traversal
+        if (acc_depth.count(i)) {  // LISTACC step (the ray's padding), then its tree in pre-order
+          emit(kListAcc, CopyRecords(src, 2, lind), 0);
+          uint32_t root;
+          memcpy(&root, &out.nodes[4 * (size_t)src + 7], 4);
+          return LinearizeAcc(root, lin, lind);
+        }
         for (int c : o.children)
           if (!Linearize(c, parent_xf, lin, lind, xf_depth)) return false;
         return true;
@@ -344,11 +385,12 @@ struct Flattener {
         return true;
       }
       case kMedium: {
+        if (ContainsAccList(o.child)) return false;  // boundary copies hold plain lists only
         uint32_t off = CopyRecords(src, kMediumRecords, lind);
         uint32_t b = CopyBoundary(o.child, lind);
         lind[4 * off + 2] = Bits(b);
         emit(kMedium, off, 0);
-        return lin.size() / 4 <= (size_t)kLinearMaxSteps;
+        return lin.size() / 4 <= LinearMaxSteps();
       }
       case kQuad: {
         uint32_t off = CopyRecords(src, kQuadRecords, lind);
@@ -368,11 +410,11 @@ struct Flattener {
           lind[4 * (off + 3) + 3] = Bits(parent_xf);  // enclosing transform of this occurrence
         }
         emit(kQuad, off, 0);
-        return lin.size() / 4 <= (size_t)kLinearMaxSteps;
+        return lin.size() / 4 <= LinearMaxSteps();
       }
       default:  // sphere
         emit(kSphere, CopyRecords(src, kSphereRecords, lind), 0);
-        return lin.size() / 4 <= (size_t)kLinearMaxSteps;
+        return lin.size() / 4 <= LinearMaxSteps();
     }
   }
 
@@ -524,7 +566,7 @@ bool CompileScene(const Scene& s, CompiledScene& out, std::string& err, bool acc
     size_t n = out.lin.size() / 4;
     std::vector<char> entry(n + 1, 0);
     for (size_t i = 0; i < n; i++)
-      if (out.lin[4 * i] == kBvh) entry[out.lin[4 * i + 1]] = 1;
+      if (out.lin[4 * i] == kBvh || out.lin[4 * i] == kAccBvh) entry[out.lin[4 * i + 1]] = 1;
     for (size_t i = n; i-- > 0;) {
       if (out.lin[4 * i] != kQuad) continue;
       uint32_t run = 1;
@@ -556,6 +598,7 @@ bool CompileScene(const Scene& s, CompiledScene& out, std::string& err, bool acc
   if (out.spheres) out.features |= kFeatSphere;
   if (out.media) out.features |= kFeatMedium;
   if (out.xforms) out.features |= kFeatXform;
+  if (out.acc_lists) out.features |= kFeatAccList;
   for (const MaterialDesc& m : s.materials)
     if (m.type == kMatMetal || m.type == kMatDielectric) out.features |= kFeatSpecular;
   for (const TextureDesc& t : s.textures) {

@@ -77,6 +77,9 @@ constexpr int kBlock = 256;
 #ifndef RT2_MIN_WAVES_VOL
 #define RT2_MIN_WAVES_VOL 6
 #endif
+#ifndef RT2_MIN_WAVES_B2LIN
+#define RT2_MIN_WAVES_B2LIN 7  // book 2 threaded: 3/4/5/6/7/8 waves 934/938/1091/1183/1297/508 Mray/s
+#endif
 #ifndef RT2_MIN_WAVES_ALL
 #define RT2_MIN_WAVES_ALL 6
 #endif
@@ -895,6 +898,12 @@ __device__ __forceinline__ bool trace_stack(const RenderParams& P, const Nodes<k
 // index, so the step kind is wave-uniform (no divergence between kinds) and the step's program
 // entry and record are scalar loads into SGPRs. A lane whose AABB test misses jumps to the node's
 // skip index. Per lane the visit order is exactly the stack traversal's.
+// the 16 words of step i (entry + first 48 record bytes) for the accelerated-list steps
+#if RT2_WIDE_PROGRAM
+#define RT2_STEP_WORDS(w) const u32x16& w = sw
+#else
+#define RT2_STEP_WORDS(w) const u32x16 w = sld16(P.lin_wide, i * 64u)
+#endif
 template <uint32_t F, bool kStats>
 __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd, float time, Path& path, HitRef& h,
                                              Counters& cnt) {
@@ -912,6 +921,8 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
   float tmax = FLT_MAX;
   uint32_t prim = kRefNone;  // closest primitive so far (h.xf: its transform, quads: from the record)
   uint32_t cur_xf = kRefNone;
+  float acc_pad = 0.0f;          // accelerated list: this ray's box padding
+  uint32_t acc_best = kRefNone;  // accelerated list: child index of its current closest sphere
   uint32_t next = 0;  // this lane's next step
   const uint32_t len = P.lin_len;
   RT2_WAVE(0);
@@ -1041,6 +1052,39 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
         ray_in_space(N, cur_xf, wo, wd, o, d);
         inv = recip3(d);
         fin = finite3(inv);
+      }
+    } else if (Has<F, kFeatAccList>() && kind == kListAcc) {
+      RT2_STEP_WORDS(aw);
+      // an accelerated HittableList (rt2_layout.h LISTACC): this ray's box padding; its tree's
+      // steps follow in pre-order, near child first
+      if (kStats) cnt.list++;
+      const f3 dc = o - mk(uf(aw[4]), uf(aw[5]), uf(aw[6]));
+      const float L = sqrtf(dot(dc, dc)) * 1.0001f + uf(aw[7]);
+      acc_pad = (uf(aw[8]) * L + uf(aw[9])) * L + uf(aw[10]);
+      acc_best = kRefNone;
+    } else if (Has<F, kFeatAccList>() && kind == kAccBvh) {
+      RT2_STEP_WORDS(aw);
+      if (kStats) cnt.bvh++;
+      // padded slab test as in trace_stack; a miss skips the subtree
+      const float ax = ((uf(aw[4]) - acc_pad) - o.x) * inv.x, bx = ((uf(aw[8]) + acc_pad) - o.x) * inv.x;
+      const float ay = ((uf(aw[5]) - acc_pad) - o.y) * inv.y, by = ((uf(aw[9]) + acc_pad) - o.y) * inv.y;
+      const float az = ((uf(aw[6]) - acc_pad) - o.z) * inv.z, bz = ((uf(aw[10]) + acc_pad) - o.z) * inv.z;
+      const float t0 = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), tmin));
+      const float t1 = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), tmax));
+      if (!(t0 <= t1)) next = st.y;
+    } else if (Has<F, kFeatAccList>() && kind == kAccSphere) {
+      RT2_STEP_WORDS(aw);
+      // smallest root wins; an equal root goes to the lower child index (aux = the child's
+      // record offset in the node array, which is list order)
+      if (kStats) cnt.sphere++;
+      float t;
+      if (sphere_t_rec(make_float4(uf(aw[4]), uf(aw[5]), uf(aw[6]), uf(aw[7])),
+                       make_float4(uf(aw[8]), uf(aw[9]), uf(aw[10]), uf(aw[11])), o, d, time, tmin, FLT_MAX, t) &&
+          (t < tmax || (t == tmax && acc_best != kRefNone && st.w < acc_best))) {
+        tmax = t;
+        prim = make_ref(kSphere, off);
+        h.xf = cur_xf;
+        acc_best = st.w;
       }
     } else if (Has<F, kFeatMedium>() && kind == kMedium) {
       if (kStats) cnt.medium++;
@@ -1243,9 +1287,10 @@ __device__ __forceinline__ uint32_t local_index(const RenderParams& P, uint32_t 
 template <uint32_t F, int kMode, bool kStats>
 constexpr int MinWaves() {
   if (RT2_MIN_WAVES_PER_EU > 0) return RT2_MIN_WAVES_PER_EU;
-  constexpr uint32_t kBook2 = kFeatSphere | kFeatMedium | kFeatXform | kFeatNoise | kFeatSpecular;
+  constexpr uint32_t kBook2 = kFeatSphere | kFeatMedium | kFeatXform | kFeatNoise | kFeatSpecular | kFeatAccList;
   if ((F == kFeatAll || F == kBook2) && !kStats && (kMode == kModeStackGlobal || kMode == kModeStackHybrid))
     return RT2_MIN_WAVES_ALL;  // book 2
+  if (F == kBook2 && !kStats && kMode == kModeLinear) return RT2_MIN_WAVES_B2LIN;
   if (kStats || kMode != kModeLinear) return 1;
   if (F == kFeatXform) return 7;                  // Cornell: 72 VGPRs
   if (F == (kFeatXform | kFeatMedium)) return RT2_MIN_WAVES_VOL;  // Cornell volume: 89 VGPRs at 5
@@ -1592,7 +1637,7 @@ constexpr uint32_t kVariants[] = {
     kFeatXform,                                   // Cornell box
     kFeatXform | kFeatMedium,                     // Cornell volume
     kFeatSphere | kFeatSpecular | kFeatDefocus,   // RTIOW book 1
-    kFeatSphere | kFeatMedium | kFeatXform | kFeatNoise | kFeatSpecular,  // RTNW book 2
+    kFeatSphere | kFeatMedium | kFeatXform | kFeatNoise | kFeatSpecular | kFeatAccList,  // RTNW book 2
     kFeatAll,                                     // everything (scene graphs, checker textures)
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);

@@ -96,7 +96,8 @@ enum Feature : uint32_t {
   kFeatSpecular = 1u << 5,  // Metal / Dielectric materials
   kFeatDefocus = 1u << 6,   // thin-lens camera (defocus_angle > 0)
   kFeatGenList = 1u << 7,   // lists whose children are not all quads/spheres (pushed on the stack)
-  kFeatAll = 0xFFu,
+  kFeatAccList = 1u << 8,   // accelerated sphere lists (LISTACC)
+  kFeatAll = 0x1FFu,
 };
 constexpr int kLdsSceneBytesMax = 96 * 1024;  // scenes up to this size are staged in LDS
 
@@ -110,12 +111,19 @@ constexpr int kLdsSceneBytesMax = 96 * 1024;  // scenes up to this size are stag
 //   kind kXform: enter the transform (record = XFORM record, skip = index of its kXformExit);
 //     the kernel walks the steps up to the exit in a nested loop with the transformed ray
 //   kind kXformExit: leave it (record = XFORM record, aux = parent XFORM ref or kRefNone)
+//   kind kListAcc: an accelerated list (record = LISTACC): sets the ray's box padding; its tree
+//     follows in pre-order, near child first: kind kAccBvh (record = ACCBVH, skip = index after
+//     the subtree, padded box test) and kind kAccSphere (record = SPHERE, aux = the sphere's
+//     record offset in the node array, i.e. its list position, for the equal-root rule)
 // Lists vanish (their children follow each other); span-1 leaves with a medium appear twice.
 // Record offsets refer to a separate record stream (RenderParams::lind) holding each step's
 // record in program order, so a run of quads is contiguous.
 // All lanes of a wave walk this array in lockstep at the smallest pending index, so the step
 // kind is wave-uniform and its record is read with scalar loads.
-constexpr int kLinearMaxSteps = 1024;  // scenes whose program is longer use the stack traversal
+// Scenes whose program is longer use the stack traversal. Measured (1920x1080, 64 spp): sphere
+// fields of 2,000 / 10,000 spheres run 1.72x / 1.37x faster threaded than stacked, 100,000 (about
+// 200 k steps) 0.97x; book 2 (accelerated list threaded as well) 1.20x.
+constexpr int kLinearMaxSteps = 1 << 16;
 #ifndef RT2_LINEAR_MAX_RUN
 #define RT2_LINEAR_MAX_RUN 10
 #endif

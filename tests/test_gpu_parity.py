@@ -155,10 +155,14 @@ def test_every_traversal_mode_matches(have_gpu, monkeypatch, mode, name, w, h, s
     assert np.array_equal(acc.view(np.uint32), o_acc.view(np.uint32))
 
 
-def test_list_acceleration_matches_linear_child_loop(have_gpu, monkeypatch):
+@pytest.mark.parametrize("mode", ["linear", "stack_lds"])
+def test_list_acceleration_matches_linear_child_loop(have_gpu, monkeypatch, mode):
     """Book 2's 1000-sphere HittableList (HittableList.cpp:8-22) through its exact acceleration tree
     gives bit-identical renders and ray counts to the reference's linear child loop, with far
-    fewer sphere tests."""
+    fewer sphere tests, in the threaded program (tree in pre-order, near child first) and in the
+    stack traversal (near child first per ray)."""
+    for k, v in MODES[mode].items():
+        monkeypatch.setenv(k, v)
     name, w, h, spp, frames = "book2_final_scene_10000_samples", 200, 200, 10000, 4
     a1, r1, s1, _ = gpu_render(name, w, h, spp, frames, stats=True)
     monkeypatch.setenv("RT2_NO_LIST_ACCEL", "1")
@@ -171,9 +175,24 @@ def test_list_acceleration_matches_linear_child_loop(have_gpu, monkeypatch):
     assert s1["sphere_tests"] * 5 < s2["sphere_tests"], (s1["sphere_tests"], s2["sphere_tests"])
 
 
-def test_generated_stress_scene(have_gpu, tmp_path):
-    """A scene from the authoring module (3000 random spheres: stack traversal over a global-memory
-    scene) is bit-identical to the oracle too."""
+def test_book2_threaded_equals_stack(have_gpu, monkeypatch):
+    """Book 2 (accelerated list, media, transforms, motion, noise) renders bit-identically in the
+    threaded program and in the stack traversal, ray counts included."""
+    args = ("book2_final_scene_10000_samples", 160, 160, 10000, 3)
+    a1, r1, s1, _ = gpu_render(*args)
+    monkeypatch.setenv("RT2_NO_LINEAR", "1")
+    a2, r2, s2, _ = gpu_render(*args)
+    assert s1["overflow"] == 0 and s2["overflow"] == 0
+    np.testing.assert_array_equal(r1, r2)
+    assert np.array_equal(a1.view(np.uint32), a2.view(np.uint32))
+
+
+@pytest.mark.parametrize("mode", ["linear", "stack_global"])
+def test_generated_stress_scene(have_gpu, tmp_path, monkeypatch, mode):
+    """A scene from the authoring module (3000 random spheres, a 6 k-step threaded program; or the
+    stack traversal over a global-memory scene) is bit-identical to the oracle too."""
+    for k, v in MODES[mode].items():
+        monkeypatch.setenv(k, v)
     import random
     from raytrace2_amd import authoring as A
     p = str(tmp_path / "field.json")

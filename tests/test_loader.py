@@ -49,9 +49,9 @@ def test_scene_compile_facts():
     assert b1.legacy_schema == 1 and b1.spheres == 484 and b1.bvh_nodes == 511  # 484 leaves -> depth-9 tree
     b2 = R.Scene(scene_path("book2_final_scene_10000_samples")).info()
     assert b2.spheres == 1007 and b2.xforms == 1 and b2.media == 2 and b2.quads == 400 * 6 + 1
-    # the 1000-sphere list under the transform gets an exact acceleration tree (n - 1 nodes) and
-    # the scene takes the stack traversal; small scenes keep the threaded program
-    assert (b2.acc_lists, b2.acc_nodes, b2.linear_steps) == (1, 999, 0)
+    # the 1000-sphere list under the transform gets an exact acceleration tree (n - 1 nodes), threaded
+    # into the program after its LISTACC step: 1 + 999 + 1000 of the program's 4922 steps
+    assert (b2.acc_lists, b2.acc_nodes, b2.linear_steps) == (1, 999, 4922)
     assert b2.max_stack <= 24
     assert info.acc_lists == 0 and info.linear_steps > 0
 
