@@ -1,20 +1,30 @@
 #!/usr/bin/env python3
 """Benchmark: Mray/s (samples x bounces) on the Cornell box at 1024^2 @ 1000 spp (BASELINE.json configs[1]).
 
-One step = one full progressive render of the workload on the rank's share of the image:
-Reset() + spp x Update() (executed as kernel launches of --launch-frames frames each) + the RCCL
-gather of every rank's row bands to rank 0 and the de-interleave there. Rays = closest-hit
-queries issued by RayColor (one per bounce level with depth > 0), counted by the
-kernel. Inputs (scene program) are resident in HBM before timing starts.
+One step = one full progressive render of the workload: Reset() + spp x Update() (launched as one
+render, rt2.h lazy queue) + the gather of every GPU's row bands into the full image on the root GPU.
+Rays = closest-hit queries issued by RayColor (one per bounce level with depth > 0),
+counted by the kernel. The scene program is resident in HBM before timing starts.
 
-  python bench.py [--gpus N --steps K --warmup W]      (N > 1: launched by torch.distributed.run)
+  python bench.py [--gpus N --steps K --warmup W]
 
-Rank 0 prints one JSON line (contract in the task statement) with a `roofline` object for the
-render kernel (algorithmic bytes per launch / HIP-event launch time vs 8 TB/s HBM) and a
-`cpu_baseline` object (the oracle restatement timed on this host's cores on a bounded sample).
+Multi-GPU goes through the C ABI (include/rt2.h), not torch:
+  * under torch.distributed.run (WORLD_SIZE = N): one process per GPU, rt2_tracer_join (partition +
+    ncclCommInitRank; the id is broadcast over a gloo control-plane group) and rt2_tracer_gather
+    (ncclGather of the row bands + de-interleave on rank 0) every step;
+  * plain `python bench.py --gpus N`: one process driving N GPUs, rt2_tracer_create_multi
+    (ncclCommInitAll); N = 1 is the same path with a communicator of size 1.
+  * --emulate-world N [--emulate-rank r|all]: diagnostic, one GPU renders rank r's bands of an N-way
+    split (all: every rank in turn); no gather.
+
+Rank 0 prints one JSON line (contract in the task statement) with a `roofline` object for the render
+kernel (bound: VALU issue; PMC instruction density from a committed profile of this kernel build and
+config x the live rays / HIP-event launch time) and a `cpu_baseline` object (the oracle restatement
+on every host core this process may use, bounded sample).
 """
 import argparse
 import glob
+import hashlib
 import json
 import os
 import sys
@@ -27,12 +37,25 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402  (import before raytrace2_amd: one HIP runtime per process)
 import torch.distributed as dist  # noqa: E402
 
-HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
-FP32_VALU_PEAK_TFLOPS = 157.3
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP32_VALU_PEAK_TFLOPS = 157.3  # spec, FMA = 2 flops
+MAX_CLOCK_HZ = 2.4e9           # MI355X_MICROARCH.md "Max clock"
+SIMDS = 256 * 4
+# VALU issue peak: a wave64 VALU instruction occupies a 32-lane SIMD for 2 cycles
+VALU_PEAK_TLANE_OPS = SIMDS * 32 * MAX_CLOCK_HZ / 1e12  # 78.64 T lane-ops/s
 # Record sizes of the flattened scene program (rt2_layout.h) in bytes
 REC_BYTES = {"bvh_tests": 32, "quad_tests": 80, "sphere_tests": 32, "xform_visits": 128, "medium_tests": 16,
              "list_visits": 16}
 FLOPS = {"bvh_tests": 18, "quad_tests": 45, "sphere_tests": 30, "xform_visits": 45, "medium_tests": 20}
+KERNEL_SOURCES = ["raytrace2_amd/csrc/render.hip", "raytrace2_amd/csrc/rt2_layout.h"]
+
+
+def kernel_sha() -> str:
+    """Identity of the render kernel build: a profile only describes the source it was taken on."""
+    h = hashlib.sha1()
+    for f in KERNEL_SOURCES:
+        h.update(open(os.path.join(ROOT, f), "rb").read())
+    return h.hexdigest()[:12]
 
 
 def parse():
@@ -52,8 +75,10 @@ def parse():
                     help="work items (pixel x frame chunk) per resident lane (-1: library default, 0: no split)")
     ap.add_argument("--batch-max", type=int, default=0, help="work items a wave reserves at once (0: default)")
     ap.add_argument("--sample-budget-gb", type=float, default=0.0, help="per-frame sample buffer bound (0: default)")
+    ap.add_argument("--plain", action="store_true", help="one GPU, no gather (the one-GPU tracer alone)")
     ap.add_argument("--emulate-world", type=int, default=1,
-                    help="diagnostic: render only rank 0's row bands of an N-GPU split on this one GPU (no gather)")
+                    help="diagnostic: render one rank's row bands of an N-GPU split on this one GPU (no gather)")
+    ap.add_argument("--emulate-rank", default="0", help="rank to emulate, or 'all' (each rank timed in turn)")
     ap.add_argument("--cpu-frames", type=int, default=48, help="oracle sample: frames at full resolution")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--stats-frames", type=int, default=8)
@@ -61,22 +86,139 @@ def parse():
     return ap.parse_args()
 
 
+def host_cores():
+    """Cores this process may run on, and the host's logical / physical counts (lscpu-equivalent)."""
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count() or 1
+    logical, phys = 0, set()
+    try:
+        pid = cid = None
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("processor"):
+                logical += 1
+            elif line.startswith("physical id"):
+                pid = line.split(":")[1].strip()
+            elif line.startswith("core id"):
+                cid = line.split(":")[1].strip()
+                phys.add((pid, cid))
+    except OSError:
+        pass
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = round(int(q) / int(period), 2)
+    except (OSError, ValueError):
+        pass
+    return {"usable": usable, "logical": logical or usable, "physical": len(phys) or None, "cgroup_cpu_quota": quota}
+
+
+def find_profile(key):
+    """The newest committed profile summary taken on this exact config and kernel build."""
+    best, stale = None, None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json")), reverse=True):
+        try:
+            prof = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        k = prof.get("key") or {}
+        if k.get("workload") != key["workload"] or k.get("partition") != key["partition"]:
+            continue
+        if "per_ray" not in prof:
+            continue
+        if k.get("kernel_sha") == key["kernel_sha"]:
+            return os.path.relpath(f, ROOT), prof, False
+        if stale is None:
+            stale = (os.path.relpath(f, ROOT), prof, True)
+    return stale if stale else (best, None, False)
+
+
+def roofline_for(tr, rays_local, launches, kernel_ms, key, rank_stats_frames, spp_total):
+    """Roofline of the render kernel on this GPU: bound = VALU issue (the kernel is issue bound,
+    DESIGN.md §4 Roofline). `achieved` = VALU lane-operations per second = the VALU instructions per
+    ray of the matching PMC profile x this run's rays per launch / this run's HIP-event launch time.
+    Also: the HBM fraction (profile traffic per ray, same scaling), the §8(d) useful-flop fraction
+    and the scene-record rate (bytes of records touched per ray / launch time, not an HBM figure)."""
+    tr.enable_stats(True)
+    tr.Reset()
+    tr.reset_stats()
+    tr.Render(rank_stats_frames)
+    s2 = tr.stats()
+    tr.enable_stats(False)
+    per_ray = {k: s2[k] / max(1, s2["rays"]) for k in REC_BYTES}
+    b_ray = sum(REC_BYTES[k] * per_ray[k] for k in REC_BYTES)
+    f_ray = sum(FLOPS.get(k, 0) * per_ray[k] for k in REC_BYTES)
+    rays_per_launch = rays_local / max(1, launches)
+    avg_launch_s = kernel_ms / 1e3 / max(1, launches)
+    src, prof, stale = find_profile(key)
+    out = {"bound": "valu_issue", "unit": "Tlane-op/s", "peak": round(VALU_PEAK_TLANE_OPS, 2),
+           "achieved": None, "frac": None, "traffic": None, "traffic_unit": "HBM bytes per launch (PMC)",
+           "kernel": "rt2::dev::render_kernel<..., false>", "avg_launch_ms": round(avg_launch_s * 1e3, 3),
+           "rays_per_launch": int(rays_per_launch), "profile": src, "profile_stale": stale}
+    if prof:
+        pr = prof["per_ray"]
+        valu = pr["valu_insts"] * rays_per_launch  # wave instructions per launch
+        out["achieved"] = round(valu * 64 / avg_launch_s / 1e12, 3)
+        out["frac"] = round(out["achieved"] / VALU_PEAK_TLANE_OPS, 4)
+        out["valu_insts_per_ray"] = round(pr["valu_insts"], 3)
+        out["salu_insts_per_ray"] = round(pr.get("salu_insts", 0.0), 3)
+        if pr.get("hbm_bytes") is not None:
+            out["traffic"] = int(pr["hbm_bytes"] * rays_per_launch)
+            out["hbm_frac"] = round(out["traffic"] / avg_launch_s / 1e9 / HBM_PEAK_GBS, 4)
+        out["profile_kernel_sha"] = (prof.get("key") or {}).get("kernel_sha")
+    out["useful_flop_frac"] = round(rays_per_launch * f_ray / avg_launch_s / 1e12 / FP32_VALU_PEAK_TFLOPS, 4)
+    frame_bytes = 12 * spp_total  # the float3 sample store per (pixel, frame), per launch below
+    out["record_rate_gbs"] = round((rays_per_launch * b_ray) / avg_launch_s / 1e9, 1)
+    out["record_bytes_per_ray"] = round(b_ray, 1)
+    out["records_per_ray"] = {k: round(v, 3) for k, v in per_ray.items()}
+    out["sample_store_bytes_per_launch"] = frame_bytes
+    return out
+
+
+def cpu_baseline(a, scene_file):
+    from oracle.oracle import OracleScene
+    cores = host_cores()
+    # every core this process may use: its affinity set, bounded by a cgroup CPU quota when one is
+    # set (more threads than the quota only time-slice the same CPUs)
+    threads = cores["usable"]
+    if cores["cgroup_cpu_quota"]:
+        threads = max(1, min(threads, int(-(-cores["cgroup_cpu_quota"] // 1))))
+    o = OracleScene(scene_file, a.seed)
+    tc = time.perf_counter()
+    _, _, cnt = o.render(a.width, a.height, a.spp, a.cpu_frames, max_depth=a.max_depth, threads=threads,
+                         forward=False)
+    dt = time.perf_counter() - tc
+    return {"value": round(cnt["rays"] / dt / 1e6, 3), "unit": "Mray/s", "cores": threads, "kind": "port",
+            "host_cores": cores,
+            "sample": f"{a.scene} {a.width}x{a.height}, frames 0..{a.cpu_frames - 1} of the spp={a.spp} "
+                      f"stratification, oracle restatement (recursive RayColor), {threads} std::threads, "
+                      f"{cnt['rays']} rays in {dt:.2f} s"}
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    # RT2_BENCH_BACKEND=gloo + RT2_BENCH_SHARE_GPU=1: rehearsal of the N-rank flow with every rank
-    # on GPU 0 and the gather over gloo through host memory (the real run is RCCL, one GPU per rank)
-    backend = os.environ.get("RT2_BENCH_BACKEND", "nccl")
-    if os.environ.get("RT2_BENCH_SHARE_GPU") == "1":
-        local_rank = 0
+    share = os.environ.get("RT2_BENCH_SHARE_GPU") == "1"  # rehearsal: every rank on GPU 0, gather via gloo
     if world > 1:
-        torch.cuda.set_device(local_rank)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-        else:
-            dist.init_process_group(backend)
+        mode = "ranks"
+        if a.gpus not in (1, world):
+            raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}")
+        n_gpus = world
+        dist.init_process_group("gloo")  # control plane only: id broadcast, barriers, max-over-ranks
+        if share:
+            local_rank = 0
+    elif a.emulate_world > 1:
+        mode, n_gpus = "emulate", 1
+    elif a.plain:
+        mode, n_gpus = "plain", 1
+    else:
+        mode, n_gpus = "multi", a.gpus
+        if torch.cuda.device_count() < n_gpus:
+            raise SystemExit(f"bench.py: --gpus {n_gpus} but {torch.cuda.device_count()} GPU(s) visible")
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
 
@@ -91,18 +233,24 @@ def main():
         authoring.GENERATORS[gen](random.Random(int(gseed)), int(n)).dump(scene_file)
     t0 = time.perf_counter()
     sc = R.Scene(scene_file, a.seed)
-    tr = R.RayTracer(sc, local_rank)
-    # a dedicated (non-null) torch stream shared with the tracer, so torch events and RCCL calls
-    # order against the render kernels
-    stream = torch.cuda.Stream(dev)
-    torch.cuda.set_stream(stream)
-    tr.set_stream(stream.cuda_stream)
+    if mode == "multi":
+        tr = R.RayTracer(sc, devices=list(range(n_gpus)), band_h=a.band_h)
+    else:
+        tr = R.RayTracer(sc, local_rank)
     tr.set_seed(a.seed)
     tr.max_depth = a.max_depth
     tr.SetSamplesPerPixel(a.spp)
     tr.OnResize((a.width, a.height))
-    emulate = a.emulate_world if world == 1 and a.emulate_world > 1 else 1
-    tr.set_partition(a.band_h, rank, world * emulate)
+    host_gather = None
+    if mode == "ranks":
+        if share:  # rehearsal only: RCCL cannot put two ranks on one GPU
+            from raytrace2_amd.dist import BandGather
+            tr.set_partition(a.band_h, rank, world)
+            host_gather = BandGather(a.height, a.width, a.band_h, world, rank, torch.device("cpu"))
+        else:
+            uid = [R.comm_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            tr.join(uid[0], world, rank, a.band_h)
     if a.launch_frames:
         tr.set_launch_frames(a.launch_frames)
     if a.work_split >= 0:
@@ -113,143 +261,104 @@ def main():
         tr.set_sample_budget(int(a.sample_budget_gb * (1 << 30)))
     tr.synchronize()
     setup_s = time.perf_counter() - t0
-    rows = tr.local_rows()
-    from raytrace2_amd.dist import BandGather
-    host_gather = world > 1 and backend != "nccl"
-    gath = (BandGather(a.height, a.width, a.band_h, world, rank, torch.device("cpu") if host_gather else dev)
-            if emulate == 1 else None)
-    assert gath is None or gath.local_view().shape[0] == rows
 
     def step():
         tr.Reset()
         tr.Render(a.spp)
         tr.flush()  # launch now: Render() only queues frames until a readback (rt2.h)
-        if gath is not None:
-            if host_gather:
-                gath.local_view().copy_(torch.from_numpy(tr.Accumulation()))
-            else:
-                tr.copy_accum_to(gath.send.data_ptr(), stream.cuda_stream)
-            gath.gather()  # RCCL gather of the row bands to rank 0 + de-interleave
+        if host_gather is not None:
+            host_gather.local_view().copy_(torch.from_numpy(tr.Accumulation()))
+            host_gather.gather()
+        elif mode in ("ranks", "multi"):
+            tr.gather()  # ncclGather of the row bands to rank 0 + de-interleave (rt2_tracer_gather)
 
-    for _ in range(a.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    tr.reset_stats()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    t_start = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(a.steps):
-        step()
-    ev1.record(stream)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t_start
-    st = tr.stats()
-    shape = tr.last_launch()
-    stream_ms = ev0.elapsed_time(ev1)
-    rays_local = st["rays"]
-    kernel_ms = st["kernel_ms"]
-    launches = max(1, st["launches"])
-    if world > 1:
-        t = torch.tensor([elapsed, float(rays_local)], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
-        tmax = t.clone()
-        dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
-        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
-        elapsed = float(tmax[0])
-        rays_total = float(t[1])
-    else:
-        rays_total = float(rays_local)
+    def sync_all():
+        if mode == "multi":
+            for d in range(n_gpus):
+                torch.cuda.synchronize(d)
+        else:
+            torch.cuda.synchronize(dev)
 
-    if rank == 0 and a.out_image and gath is not None:
-        img = gath.image.cpu().numpy() / np.float32(a.spp)
-        R.WriteImage(img, a.width, a.height, a.out_image)
+    def timed(steps, warmup):
+        for _ in range(warmup):
+            step()
+        sync_all()
+        tr.reset_stats()
+        if mode == "ranks":
+            dist.barrier()
+        sync_all()
+        t_start = time.perf_counter()
+        for _ in range(steps):
+            step()
+        sync_all()
+        if mode == "ranks":
+            dist.barrier()
+        return time.perf_counter() - t_start, tr.stats()
+
+    ranks_to_run = [0]
+    if mode == "emulate":
+        ranks_to_run = list(range(a.emulate_world)) if a.emulate_rank == "all" else [int(a.emulate_rank)]
+    per_rank = []
+    for er in ranks_to_run:
+        if mode == "emulate":
+            tr.set_partition(a.band_h, er, a.emulate_world)
+        el, st = timed(a.steps, a.warmup)
+        per_rank.append({"rank": er, "rows": tr.local_rows(), "elapsed_s": el, "rays": st["rays"],
+                         "kernel_ms": st["kernel_ms"], "launches": st["launches"], "gather_ms": st["gather_ms"],
+                         "gathers": st["gathers"], "mray_s": st["rays"] / el / 1e6})
+    me = per_rank[-1] if mode != "emulate" else max(per_rank, key=lambda r: r["elapsed_s"])
+    if mode == "ranks":
+        gathered = [None] * world
+        dist.all_gather_object(gathered, per_rank[0] | {"rank": rank})
+        per_rank = gathered
+    elapsed = max(r["elapsed_s"] for r in per_rank)
+    rays_total = float(sum(r["rays"] for r in per_rank))
+
+    if rank == 0 and a.out_image and mode != "emulate":
+        img = (tr.image_accumulation() if mode != "plain" and host_gather is None else
+               (host_gather.image.numpy() if host_gather is not None else tr.Accumulation()))
+        R.WriteImage(img / np.float32(a.spp), a.width, a.height, a.out_image)
 
     workload = f"{a.scene} {a.width}x{a.height} @ {a.spp} spp, max_depth {a.max_depth}"
-    # ---- algorithmic bytes per ray from a stats pass (same seed, same kernel family) ----
+    if mode == "emulate":
+        partition = f"emulate {a.emulate_world}-way h={a.band_h} rank {me['rank']}"
+    elif n_gpus > 1:
+        partition = f"{n_gpus}-way h={a.band_h} rank 0"
+    else:
+        partition = "1 GPU"
+    key = {"workload": workload, "partition": partition, "kernel_sha": kernel_sha()}
     roofline = None
-    if rank == 0:
-        tr.enable_stats(True)
-        tr.Reset()
-        tr.reset_stats()
-        tr.Render(a.stats_frames)
-        s2 = tr.stats()
-        tr.enable_stats(False)
-        per_ray = {k: s2[k] / max(1, s2["rays"]) for k in REC_BYTES}
-        b_ray = sum(REC_BYTES[k] * per_ray[k] for k in REC_BYTES)
-        f_ray = sum(FLOPS.get(k, 0) * per_ray[k] for k in REC_BYTES)
-        rays_per_launch = rays_local / launches
-        pixels_local = rows * a.width
-        frame_bytes = pixels_local * 12 * (a.spp * a.steps / launches)  # float3 sample store per frame
-        bytes_per_launch = rays_per_launch * b_ray + frame_bytes
-        avg_launch_s = kernel_ms / 1e3 / launches
-        achieved = bytes_per_launch / avg_launch_s / 1e9
-        traffic, traffic_src, valu_issue = None, None, None
-        for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json")), reverse=True):
-            try:
-                prof = json.load(open(f))
-                under = prof.get("bench_under_rocprof") or {}
-                if under.get("config", {}).get("workload") != workload or "hbm_bytes_per_launch" not in prof:
-                    continue
-                traffic = int(prof["hbm_bytes_per_launch"]["corrected"])
-                traffic_src = os.path.relpath(f, ROOT)
-                pmc = prof.get("pmc", {})
-                if "SQ_INSTS_VALU" in pmc and "GRBM_GUI_ACTIVE" in pmc:
-                    ms = pmc["dispatch_ms"]["pmc_SQ_WAVES_SQ_INSTS_VALU_SQ_INSTS_SALU_SQ_"]
-                    clock = pmc["GRBM_GUI_ACTIVE"] / 8 / (ms / 1e3)  # MI355X_MICROARCH.md: sum over 8 XCDs
-                    simds = 4 * 256
-                    valu_issue = pmc["SQ_INSTS_VALU"] * 2 / (simds * clock * ms / 1e3)  # wave64 = 2 cycles/SIMD32
-                break
-            except (OSError, ValueError, KeyError):
-                continue
-        roofline = {
-            "bound": "hbm",
-            "achieved": round(achieved, 1),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": traffic,
-            "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, gfx950-corrected)",
-            "traffic_source": traffic_src,
-            "note": "algorithmic bytes = scene records touched per ray (SURVEY 8d) served from the scalar cache/L1; "
-                    "frac > 1 means that record traffic exceeds what HBM alone could feed; measured HBM traffic is "
-                    "`traffic`; the kernel is VALU-issue/latency bound (valu_issue_frac)",
-            "valu_issue_frac": None if valu_issue is None else round(valu_issue, 3),
-            "kernel": "rt2::dev::render_kernel<false>",
-            "avg_launch_ms": round(kernel_ms / launches, 3),
-            "bytes_per_ray": round(b_ray, 1),
-            "records_per_ray": {k: round(v, 3) for k, v in per_ray.items()},
-            "useful_flop_frac": round(rays_per_launch * f_ray / avg_launch_s / 1e12 / FP32_VALU_PEAK_TFLOPS, 4),
-        }
-
     cpu = None
-    if rank == 0 and not a.no_cpu and world == 1:
-        from oracle.oracle import OracleScene
-        try:
-            cores = min(16, len(os.sched_getaffinity(0)))
-        except AttributeError:
-            cores = min(16, os.cpu_count() or 1)
-        o = OracleScene(scene_file, a.seed)
-        tc = time.perf_counter()
-        _, _, cnt = o.render(a.width, a.height, a.spp, a.cpu_frames, max_depth=a.max_depth, threads=cores,
-                             forward=False)
-        dt = time.perf_counter() - tc
-        cpu = {"value": round(cnt["rays"] / dt / 1e6, 3), "unit": "Mray/s", "cores": cores, "kind": "port",
-               "sample": f"{a.scene} {a.width}x{a.height}, frames 0..{a.cpu_frames - 1} of the spp={a.spp} "
-                         f"stratification, oracle restatement (recursive RayColor), {cnt['rays']} rays in "
-                         f"{dt:.2f} s"}
+    if rank == 0:
+        if mode == "emulate":  # the slowest rank's partition
+            tr.set_partition(a.band_h, me["rank"], a.emulate_world)
+        mine = me if mode != "ranks" else per_rank[0]
+        gpu_rays, gpu_kernel_ms, launches = mine["rays"], mine["kernel_ms"], mine["launches"]
+        if mode == "multi" and n_gpus > 1:  # per-GPU share (kernel_ms is the busiest GPU's)
+            gpu_rays = mine["rays"] / n_gpus
+        roofline = roofline_for(tr, gpu_rays, launches, gpu_kernel_ms, key, a.stats_frames,
+                                tr.local_rows() * a.width * a.spp * a.steps // max(1, launches))
+        if not a.no_cpu:
+            cpu = cpu_baseline(a, scene_file)
 
     if rank == 0:
         value = rays_total / elapsed / 1e6
+        if mode == "ranks":
+            par = (f"row-bands h={a.band_h} x {world} GPUs, one process per GPU, "
+                   + ("host gather over gloo (rehearsal on one GPU)" if share else
+                      "RCCL ncclGather to rank 0 through the C ABI (rt2_tracer_join/gather)"))
+        elif mode == "multi":
+            par = (f"row-bands h={a.band_h} x {n_gpus} GPU(s) in one process (rt2_tracer_create_multi), "
+                   "RCCL ncclGather to GPU 0 + de-interleave")
+        elif mode == "plain":
+            par = "1 GPU, no gather (one-GPU tracer)"
+        else:
+            par = f"emulated rank(s) of a {a.emulate_world}-way row-band split on one GPU, no gather"
         out = {
             "metric": "Mray/s (samples x bounces) Cornell Box 1024^2 @ 1000 spp",
             "value": round(value, 2),
             "unit": "Mray/s",
-            "n_gpus": world,
+            "n_gpus": n_gpus,
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": round(elapsed * 1e3 / a.steps, 2),
@@ -259,26 +368,30 @@ def main():
             "dtype": "f32",
             "data": "synthetic: committed scene JSON (scenes/), Philox4x32-10 sample streams seeded "
                     f"{a.seed:#x}",
-            "config": {"workload": workload,
-                       "parallelism": f"row-bands h={a.band_h} x {world} GPU(s), RCCL gather to rank 0",
-                       "launch_frames": a.spp * a.steps // launches,
-                       "work_split": shape},
+            "config": {"workload": workload, "parallelism": par, "partition": partition,
+                       "launch_frames": a.spp * a.steps // max(1, me["launches"]),
+                       "work_split": tr.last_launch()},
             "roofline": roofline,
             "cpu_baseline": cpu,
-            "detail": {"rays": int(rays_total), "stream_ms": round(stream_ms, 2),
-                       "kernel_ms_per_step": round(kernel_ms / a.steps, 2), "launches": launches,
-                       "variant_features": hex(tr.last_variant_features()) if hasattr(tr, "last_variant_features") else None,
-                       "setup_s": round(setup_s, 3), "stamps": st.get("stamps"),
-                       "rays_per_sample": round(rays_total / (a.steps * a.spp * a.width * rows * world), 4)},
+            "detail": {"rays": int(rays_total), "launches": me["launches"], "setup_s": round(setup_s, 3),
+                       "kernel_sha": key["kernel_sha"],
+                       "kernel_ms_per_step_max": round(max(r["kernel_ms"] for r in per_rank) / a.steps, 2),
+                       "gather_ms_per_step": round(per_rank[0]["gather_ms"] / a.steps, 3),
+                       "per_rank": [{"rank": r["rank"], "rows": r["rows"], "mray_s": round(r["mray_s"], 1),
+                                     "ms_per_step": round(r["elapsed_s"] * 1e3 / a.steps, 2),
+                                     "kernel_ms_per_step": round(r["kernel_ms"] / a.steps, 2)} for r in per_rank],
+                       "rays_per_sample": round(rays_total / (a.steps * a.spp * a.width *
+                                                              sum(r["rows"] for r in per_rank)), 4)},
         }
         if cpu:
             out["detail"]["gpu_over_cpu"] = round(value / cpu["value"], 1)
-        if emulate > 1:
-            out["config"]["emulated"] = (f"rank 0 of {emulate}: {rows} of {a.height} rows on this GPU, no gather; "
-                                         "value is this GPU's rate, not a job rate")
+        if mode == "emulate":
+            out["config"]["emulated"] = (f"{len(per_rank)} rank(s) of {a.emulate_world} timed one after another on "
+                                         "this GPU; value = their rays / the slowest rank's time (no gather)")
         print(json.dumps(out), flush=True)
     tr.close()
-    if world > 1:
+    if mode == "ranks":
+        dist.barrier()
         dist.destroy_process_group()
 
 

@@ -100,7 +100,7 @@ RT2_API int rt2_settings_load(const char* path, rt2_app_settings* out);
  * `lazy_frames` (default 4096; 0 = launch at every call) are queued. Reset/OnResize drop queued
  * frames. Results are identical either way; FrameIdx() counts queued frames. Launched frames run on
  * the tracer's stream; readbacks synchronise it. */
-RT2_API int rt2_tracer_create(const rt2_scene* scene, int device, rt2_tracer** out);
+RT2_API int rt2_tracer_create(const rt2_scene* scene, int device, rt2_tracer** out); /* n GPUs: see below */
 RT2_API void rt2_tracer_destroy(rt2_tracer* tr);
 RT2_API int rt2_tracer_set_stream(rt2_tracer* tr, void* hip_stream); /* NULL = own stream */
 RT2_API int rt2_tracer_set_max_depth(rt2_tracer* tr, int max_depth); /* RayTracer::max_depth, <= 65535 */
@@ -145,6 +145,47 @@ RT2_API void rt2_host_free(void* ptr);
 /* Device-to-device copy of the local accumulation (float3 per local pixel) into `dst_device`,
  * ordered on `hip_stream` (NULL = tracer stream) — used for the multi-GPU gather. */
 RT2_API int rt2_tracer_copy_accum_device(rt2_tracer* tr, void* dst_device, void* hip_stream);
+/* ---- RayTracer::camera (RayTracer.hpp:31) ----
+ * The reference borrows `Camera* camera` (= &scene.cam, App.cpp:130) and calls camera->Update() at
+ * every Update() (RayTracer.cpp:56): a camera moved between Update() calls takes effect at the next
+ * frame and does not reset the accumulation. set_camera gives the tracer the setter fields of
+ * Camera.hpp:69-101 (center, look_at, view_up, vfov, defocus_angle, focus_distance; dims and
+ * samples_per_pixel stay as on_resize / set_samples_per_pixel set them). When they change, frames
+ * queued so far are launched first, with the camera they were queued under. */
+RT2_API int rt2_tracer_set_camera(rt2_tracer* tr, const rt2_camera_desc* cam);
+RT2_API int rt2_tracer_get_camera(const rt2_tracer* tr, rt2_camera_desc* out);
+
+/* ---- Multi-GPU; replaces the reference's data-parallel pixel loop
+ * std::for_each(std::execution::par, ...) (RayTracer.cpp:69) ----
+ * Pixels are independent and sample streams are keyed by (seed, global pixel, frame), so the image
+ * is split into interleaved row bands (band b -> GPU b % n) and rendered with no communication. The
+ * one exchange is an RCCL gather (ncclGather over xGMI) of every GPU's band stack to the root GPU,
+ * where a kernel de-interleaves it into the full image. The result is bit-identical to one GPU.
+ *
+ * (1) One process driving n GPUs: rt2_tracer_create_multi (devices NULL = 0..n-1; band_h 0 = 16),
+ *     one RCCL communicator per device (ncclCommInitAll). Every rt2_tracer_* function works on it as
+ *     on a one-GPU tracer; readbacks (accumulation, non_converted_pixels, pixels, pixels_async,
+ *     ray_counts, copy_accum_device) return the FULL image (local_rows = height), gathering first.
+ *     set_stream, set_partition and join are refused. A device listed more than once runs several
+ *     partitions on one GPU with device-local copies in place of RCCL (a test configuration).
+ * (2) One process per GPU (torchrun / MPI style): each process creates a one-GPU tracer; rank 0 makes
+ *     an id with rt2_comm_unique_id, the caller broadcasts it, and every rank calls rt2_tracer_join
+ *     (= set_partition(band_h, rank, world) + ncclCommInitRank). Readbacks stay local (the rank's
+ *     bands); rt2_tracer_gather is the collective that assembles the full image on rank 0, read
+ *     there with rt2_tracer_image_*.
+ * rt2_tracer_gather works in both modes. It is enqueued on the tracers' streams and does not wait. */
+#define RT2_UNIQUE_ID_BYTES 128
+RT2_API int rt2_tracer_create_multi(const rt2_scene* scene, int n_gpus, const int* devices, int band_h,
+                                    rt2_tracer** out);
+RT2_API int rt2_tracer_n_gpus(const rt2_tracer* tr); /* devices of a multi tracer, else 1 */
+RT2_API int rt2_comm_unique_id(uint8_t* out, size_t cap); /* cap >= RT2_UNIQUE_ID_BYTES */
+RT2_API int rt2_tracer_join(rt2_tracer* tr, const uint8_t* unique_id, int world, int rank, int band_h);
+RT2_API int rt2_tracer_gather(rt2_tracer* tr);
+/* Root (rank 0 / a multi tracer) after a gather: the full image, rows bottom-up, H x W. */
+RT2_API int rt2_tracer_image_accumulation(rt2_tracer* tr, float* out);        /* raw float3 sums */
+RT2_API int rt2_tracer_image_non_converted_pixels(rt2_tracer* tr, float* out); /* accum / frame_idx */
+RT2_API int rt2_tracer_image_pixels(rt2_tracer* tr, uint8_t* out_rgba);       /* Pixels(): RGBA8 */
+
 RT2_API int rt2_tracer_enable_ray_counts(rt2_tracer* tr, int on);
 RT2_API int rt2_tracer_ray_counts(rt2_tracer* tr, uint32_t* out); /* rays per local pixel */
 RT2_API int rt2_tracer_enable_stats(rt2_tracer* tr, int on);      /* per-record test counters */
@@ -158,6 +199,12 @@ typedef struct {
   double kernel_ms;   /* sum of per-launch HIP event durations */
   uint64_t stamps[4]; /* diagnostic builds only: s_memtime sums (fetch, trace, shade, finish) */
   uint64_t diag[8];   /* diagnostic builds only: per-wave traversal step counts */
+  /* multi-GPU (root): gathers done, and the sum of their root-stream durations (HIP events from the
+   * root's last render kernel to the de-interleaved image; waiting for the slowest GPU included).
+   * For a multi-GPU tracer the counters above are sums over its GPUs, except launches (per GPU)
+   * and kernel_ms (the largest per-GPU sum). */
+  uint64_t gathers;
+  double gather_ms;
 } rt2_stats;
 RT2_API int rt2_tracer_get_stats(rt2_tracer* tr, rt2_stats* out);
 RT2_API int rt2_tracer_reset_stats(rt2_tracer* tr);

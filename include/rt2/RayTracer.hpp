@@ -10,9 +10,11 @@
 //   serialize::LoadAppSettings                  rt2::serialize::LoadAppSettings
 //   util::WriteImage                            rt2::util::WriteImage
 //
-// Differences a caller sees: the tracer renders on a GPU (device index at construction) and owns
-// device buffers; Update() takes the scene only for signature compatibility (the scene program
-// was uploaded at construction); errors throw rt2::Error (the C ABI itself never throws).
+// Differences a caller sees: the tracer renders on GPUs (device index, or a GPU count, at
+// construction) and owns device buffers; Update() takes the scene only for signature compatibility
+// (the scene program was uploaded at construction); errors throw rt2::Error (the C ABI itself never
+// throws). With n_gpus > 1 the image is split into interleaved row bands over the GPUs and gathered
+// over RCCL before every readback (rt2_tracer_create_multi); results are identical to one GPU.
 #pragma once
 
 #include <cstdint>
@@ -158,12 +160,20 @@ inline void WriteImage(const std::vector<vec3>& pixels, int width, int height, c
 }
 }  // namespace util
 
-// cpu::RayTracer (RayTracer.hpp:15-42) on one MI355X GPU.
+// cpu::RayTracer (RayTracer.hpp:15-42) on MI355X GPUs: one GPU (`device`; n_gpus 0), or `n_gpus`
+// GPUs starting at `device` with an RCCL gather of their row bands (band_h 0 = 16 rows; n_gpus 1
+// is the same path with a communicator of size 1).
 class RayTracer {
  public:
-  RayTracer(const Scene& scene, int device = 0) {
+  explicit RayTracer(const Scene& scene, int device = 0, int n_gpus = 0, int band_h = 0) {
     rt2_tracer* t = nullptr;
-    Check(rt2_tracer_create(scene.handle(), device, &t));
+    if (n_gpus <= 0) {
+      Check(rt2_tracer_create(scene.handle(), device, &t));
+    } else {
+      std::vector<int> devs((size_t)n_gpus);
+      for (int i = 0; i < n_gpus; i++) devs[(size_t)i] = device + i;
+      Check(rt2_tracer_create_multi(scene.handle(), n_gpus, devs.data(), band_h, &t));
+    }
     t_.reset(t);
   }
 
@@ -196,10 +206,14 @@ class RayTracer {
   bool OnEvent(const void* /*sdl_event*/) { return false; }  // no window on the GPU path
   void OnImGui() {}
 
-  Camera* camera = nullptr;  // like the reference: points at scene.cam; read at each Update
+  // Like the reference (RayTracer.hpp:31-32): `camera` points at scene.cam and is read at every
+  // Update (camera->Update(), RayTracer.cpp:56), so moving it between Update() calls takes effect
+  // at the next frame; max_depth likewise.
+  Camera* camera = nullptr;
   size_t max_depth = 50;
 
   rt2_tracer* handle() const { return t_.get(); }
+  [[nodiscard]] int NumGpus() const { return rt2_tracer_n_gpus(t_.get()); }
 
  private:
   struct Deleter {
@@ -207,7 +221,11 @@ class RayTracer {
   };
   void Sync() {
     Check(rt2_tracer_set_max_depth(t_.get(), (int)max_depth));
-    if (camera) Check(rt2_tracer_set_samples_per_pixel(t_.get(), camera->samples_per_pixel_));
+    if (camera) {
+      Check(rt2_tracer_set_samples_per_pixel(t_.get(), camera->samples_per_pixel_));
+      rt2_camera_desc d = camera->Desc();
+      Check(rt2_tracer_set_camera(t_.get(), &d));
+    }
   }
   std::unique_ptr<rt2_tracer, Deleter> t_;
   ivec2 dims_;

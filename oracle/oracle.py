@@ -54,6 +54,8 @@ def lib():
         L.oracle_scene_textures.argtypes = [vp, fp, i32]
         L.oracle_scene_perlin.argtypes = [vp, i32, fp, ctypes.POINTER(ctypes.c_int)]
         L.oracle_camera_params.argtypes = [vp, i32, i32, i32, fp]
+        L.oracle_scene_set_camera.argtypes = [vp, fp]
+        L.oracle_scene_set_camera.restype = None
         L.oracle_scene_hit.argtypes = [vp, fp, fp, ctypes.c_float, ctypes.c_float, ctypes.c_float, u64, fp]
         L.oracle_philox.argtypes = [ctypes.POINTER(ctypes.c_uint32)] * 3
         L.oracle_uniforms.argtypes = [u64, ctypes.c_uint32, ctypes.c_uint32, i32, fp]
@@ -115,6 +117,12 @@ class OracleScene:
         if pc < 0:
             raise ValueError("not a noise texture")
         return vec[:pc].copy(), perm[:3 * pc].reshape(3, pc).copy()
+
+    def set_camera(self, center, look_at, view_up, vfov, defocus_angle, focus_distance) -> None:
+        """Camera setters (Camera.hpp:69-101) for the renders that follow."""
+        v = np.array(list(center) + list(look_at) + list(view_up) + [vfov, defocus_angle, focus_distance],
+                     np.float32)
+        lib().oracle_scene_set_camera(self._h, _f(v))
 
     def camera_params(self, w: int, h: int, spp: int) -> np.ndarray:
         out = np.zeros(21, np.float32)

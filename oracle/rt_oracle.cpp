@@ -1346,6 +1346,18 @@ int oracle_scene_perlin(void* sp, int tex, float* vec, int* perm) {
   return pc;
 }
 
+// Camera setters (Camera.hpp:69-101) on the scene camera the next renders use:
+// in = center(3) look_at(3) view_up(3) vfov defocus_angle focus_distance
+void oracle_scene_set_camera(void* sp, const float* in) {
+  Scene* s = (Scene*)sp;
+  s->cam.center_ = {in[0], in[1], in[2]};
+  s->cam.lookat_ = {in[3], in[4], in[5]};
+  s->cam.view_up_ = {in[6], in[7], in[8]};
+  s->cam.vfov_ = in[9];
+  s->cam.defocus_angle_ = in[10];
+  s->cam.focus_dist_ = in[11];
+}
+
 // Camera basis after Camera::Update for the given dims/spp: 6 vec3 (pixel00, du, dv, center,
 // defocus_u, defocus_v) + defocus_angle, recip_sqrt_spp, sqrt_spp.
 int oracle_camera_params(void* sp, int w, int h, int spp, float* out) {

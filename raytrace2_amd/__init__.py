@@ -6,7 +6,8 @@ package fails loudly when that library is missing; there is no CPU fallback.
 """
 from ._native import Rt2Error, declared_symbols, lib  # noqa: F401
 from .tracer import (DEFAULT_SEED, Camera, LoadAppSettings, LoadCamera, RayTracer, Scene,  # noqa: F401
-                     SceneLoader, Settings, WriteCamera, WriteImage, assemble_bands, local_rows)
+                     SceneLoader, Settings, WriteCamera, WriteImage, assemble_bands, comm_unique_id,
+                     local_rows)
 
 __all__ = ["Camera", "LoadAppSettings", "LoadCamera", "RayTracer", "Scene", "SceneLoader", "Settings",
-           "WriteCamera", "WriteImage", "assemble_bands", "local_rows", "Rt2Error", "DEFAULT_SEED"]
+           "WriteCamera", "WriteImage", "assemble_bands", "comm_unique_id", "local_rows", "Rt2Error", "DEFAULT_SEED"]

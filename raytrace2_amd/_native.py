@@ -15,6 +15,7 @@ RT2_ERR_INVALID = -1
 RT2_ERR_IO = -2
 RT2_ERR_SCENE = -3
 RT2_ERR_HIP = -4
+UNIQUE_ID_BYTES = 128  # RT2_UNIQUE_ID_BYTES
 
 
 class Rt2Error(RuntimeError):
@@ -51,10 +52,12 @@ class Stats(ctypes.Structure):
                 ("rays", "paths", "bvh_tests", "quad_tests", "sphere_tests", "xform_visits",
                  "medium_tests", "list_visits", "overflow", "launches")] + [("kernel_ms", ctypes.c_double),
                                                                            ("stamps", ctypes.c_uint64 * 4),
-                                                                           ("diag", ctypes.c_uint64 * 8)]
+                                                                           ("diag", ctypes.c_uint64 * 8),
+                                                                           ("gathers", ctypes.c_uint64),
+                                                                           ("gather_ms", ctypes.c_double)]
 
     def as_dict(self):
-        d = {n: (getattr(self, n) if n == "kernel_ms" else int(getattr(self, n))) for n, _ in self._fields_
+        d = {n: (getattr(self, n) if n in ("kernel_ms", "gather_ms") else int(getattr(self, n))) for n, _ in self._fields_
              if n not in ("stamps", "diag")}
         d["stamps"] = [int(x) for x in self.stamps]
         d["diag"] = [int(x) for x in self.diag]
@@ -134,6 +137,16 @@ def _load():
         "rt2_tracer_get_stats": (i32, [vp, ctypes.POINTER(Stats)]),
         "rt2_tracer_reset_stats": (i32, [vp]),
         "rt2_write_image": (i32, [fp, i32, i32, ctypes.c_char_p, i32]),
+        "rt2_tracer_set_camera": (i32, [vp, ctypes.POINTER(CameraDesc)]),
+        "rt2_tracer_get_camera": (i32, [vp, ctypes.POINTER(CameraDesc)]),
+        "rt2_tracer_create_multi": (i32, [vp, i32, ctypes.POINTER(ctypes.c_int), i32, pp]),
+        "rt2_tracer_n_gpus": (i32, [vp]),
+        "rt2_comm_unique_id": (i32, [ctypes.POINTER(ctypes.c_uint8), ctypes.c_size_t]),
+        "rt2_tracer_join": (i32, [vp, ctypes.POINTER(ctypes.c_uint8), i32, i32, i32]),
+        "rt2_tracer_gather": (i32, [vp]),
+        "rt2_tracer_image_accumulation": (i32, [vp, fp]),
+        "rt2_tracer_image_non_converted_pixels": (i32, [vp, fp]),
+        "rt2_tracer_image_pixels": (i32, [vp, ctypes.POINTER(ctypes.c_uint8)]),
         "rt2_selftest": (i32, [i32, i32, u64, u64, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
     }
     for name, (res, args) in sig.items():

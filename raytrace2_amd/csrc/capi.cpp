@@ -1,6 +1,9 @@
 // capi.cpp — implementation of include/rt2.h: scene handles, the device-side RayTracer and the
 // host utilities. Device memory is owned by the tracer (hipMalloc); the caller owns host buffers.
+// A multi-GPU tracer is a facade over one one-GPU tracer per device (rank i = parts[i]) plus the
+// RCCL gather of their row bands to rank 0.
 #include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cstdlib>
@@ -24,6 +27,8 @@ int RenderVariant(uint32_t features);
 uint32_t RenderVariantFeatures(int v);
 size_t RenderLdsBytes(const RenderParams& p);
 bool WriteImage(const float* pixels, int w, int h, const std::string& path, bool png, std::string& err);
+hipError_t LaunchDeinterleave(const float* stacks, float* image, uint8_t* pixels, int width, int height, int band_h,
+                              int world, int max_rows, int frame_idx, hipStream_t stream);
 }  // namespace rt2
 
 using namespace rt2;
@@ -96,6 +101,19 @@ struct rt2_tracer {
   double kernel_ms = 0;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;  // per-launch timing events
   std::vector<hipEvent_t> event_pool;
+  // ---- multi-GPU ----
+  std::vector<rt2_tracer*> parts;  // multi tracer: one one-GPU tracer per device, parts[i] = rank i
+  bool loopback = false;           // the parts share one GPU: device-local copies instead of RCCL
+  ncclComm_t comm = nullptr;       // this tracer's rank in an RCCL communicator (a part, or joined)
+  // root (rank 0) image: the gathered band stacks and the de-interleaved full image
+  float* d_stacks = nullptr;      // [world][max_rows][W] float3
+  float* d_image = nullptr;       // [H][W] float3
+  uint8_t* d_image_px = nullptr;  // [H][W] RGBA8
+  size_t stacks_bytes = 0, image_pixels = 0;
+  int64_t image_frame = -1;  // frame index of the last gather (-1: none since the last resize/reset)
+  uint64_t gathers = 0;
+  double gather_ms = 0;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> gpending;  // per-gather timing events
 };
 
 namespace {
@@ -115,11 +133,42 @@ int HipFail(hipError_t e, const char* what) {
     if (_e != hipSuccess) return HipFail(_e, #expr);   \
   } while (0)
 
+#define NCCL_TRY(expr)                                                                     \
+  do {                                                                                     \
+    ncclResult_t _r = (expr);                                                              \
+    if (_r != ncclSuccess) return Fail(RT2_ERR_HIP, std::string(#expr) + ": " + ncclGetErrorString(_r)); \
+  } while (0)
+
 int LocalRows(int h, int band_h, int rank, int world) {
   int n = 0;
   for (int y = 0; y < h; y++)
     if ((y / band_h) % world == rank) n++;
   return n;
+}
+
+int BandH(const rt2_tracer* t) { return t->band_h > 0 ? t->band_h : (t->height > 0 ? t->height : 1); }
+
+// Rows of the largest rank's band stack (every rank's accumulation is allocated this tall, so the
+// gather sends equal counts; the padding rows stay zero).
+int BandRowsMax(const rt2_tracer* t) {
+  if (t->height <= 0) return 0;
+  const int bh = BandH(t);
+  const int bands = (t->height + bh - 1) / bh;
+  return (bands + t->world - 1) / t->world * bh;
+}
+
+int AllocRows(const rt2_tracer* t) { return t->world > 1 ? BandRowsMax(t) : t->local_rows; }
+
+void FreeImage(rt2_tracer* t) {
+  (void)hipFree(t->d_stacks);
+  (void)hipFree(t->d_image);
+  (void)hipFree(t->d_image_px);
+  t->d_stacks = nullptr;
+  t->d_image = nullptr;
+  t->d_image_px = nullptr;
+  t->stacks_bytes = 0;
+  t->image_pixels = 0;
+  t->image_frame = -1;
 }
 
 void FreeFrame(rt2_tracer* t) {
@@ -132,13 +181,13 @@ void FreeFrame(rt2_tracer* t) {
   t->d_accum = nullptr;
   t->d_pixels = nullptr;
   t->d_ray_counts = nullptr;
+  FreeImage(t);
 }
 
 int Realloc(rt2_tracer* t) {
   FreeFrame(t);
-  int bh = t->band_h > 0 ? t->band_h : (t->height > 0 ? t->height : 1);
-  t->local_rows = t->height > 0 ? LocalRows(t->height, bh, t->rank, t->world) : 0;
-  size_t n = (size_t)t->width * (size_t)t->local_rows;
+  t->local_rows = t->height > 0 ? LocalRows(t->height, BandH(t), t->rank, t->world) : 0;
+  size_t n = (size_t)t->width * (size_t)AllocRows(t);
   if (n == 0) return RT2_OK;
   HIP_TRY(hipMalloc(&t->d_accum, n * 3 * sizeof(float)));
   HIP_TRY(hipMalloc(&t->d_pixels, n * 4));
@@ -147,10 +196,12 @@ int Realloc(rt2_tracer* t) {
 }
 
 int ResetFrame(rt2_tracer* t) {
-  size_t n = (size_t)t->width * (size_t)t->local_rows;
+  size_t n = (size_t)t->width * (size_t)AllocRows(t);
   t->frame_idx = 0;
   t->queued = 0;  // queued frames would only be accumulated and zeroed again
+  t->image_frame = -1;
   if (n == 0) return RT2_OK;
+  HIP_TRY(hipSetDevice(t->device));
   HIP_TRY(hipMemsetAsync(t->d_accum, 0, n * 3 * sizeof(float), t->stream));
   HIP_TRY(hipMemsetAsync(t->d_pixels, 0, n * 4, t->stream));
   if (t->d_ray_counts) HIP_TRY(hipMemsetAsync(t->d_ray_counts, 0, n * sizeof(uint32_t), t->stream));
@@ -178,6 +229,15 @@ int DrainEvents(rt2_tracer* t) {
     t->event_pool.push_back(pr.second);
   }
   t->pending.clear();
+  for (auto& pr : t->gpending) {
+    HIP_TRY(hipEventSynchronize(pr.second));
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, pr.first, pr.second));
+    t->gather_ms += ms;
+    t->event_pool.push_back(pr.first);
+    t->event_pool.push_back(pr.second);
+  }
+  t->gpending.clear();
   return RT2_OK;
 }
 
@@ -456,7 +516,18 @@ int rt2_tracer_create(const rt2_scene* s, int device, rt2_tracer** out) {
 
 void rt2_tracer_destroy(rt2_tracer* t) {
   if (!t) return;
+  if (!t->parts.empty()) {
+    for (rt2_tracer* p : t->parts) rt2_tracer_destroy(p);
+    delete t;
+    return;
+  }
   (void)hipSetDevice(t->device);
+  if (t->stream) (void)hipStreamSynchronize(t->stream);
+  if (t->comm) (void)ncclCommDestroy(t->comm);
+  for (auto& pr : t->gpending) {
+    (void)hipEventDestroy(pr.first);
+    (void)hipEventDestroy(pr.second);
+  }
   if (t->stream) (void)hipStreamSynchronize(t->stream);
   for (auto& pr : t->pending) {
     (void)hipEventDestroy(pr.first);
@@ -478,8 +549,36 @@ void rt2_tracer_destroy(rt2_tracer* t) {
   delete t;
 }
 
+}  // extern "C"
+
+namespace {
+bool IsMulti(const rt2_tracer* t) { return !t->parts.empty(); }
+
+// Applies f to every part of a multi tracer (stops at the first error).
+template <typename Fn>
+int ForParts(rt2_tracer* t, Fn&& f) {
+  for (rt2_tracer* p : t->parts) {
+    int rc = f(p);
+    if (rc != RT2_OK) return rc;
+  }
+  return RT2_OK;
+}
+
+// Forwards a setter to every part of a multi tracer.
+#define RT2_FORWARD(t, call)                                           \
+  do {                                                                 \
+    if (IsMulti(t)) return ForParts(t, [&](rt2_tracer* p) { return call; }); \
+  } while (0)
+}  // namespace
+
+extern "C" {
+
 int rt2_tracer_set_stream(rt2_tracer* t, void* s) {
   if (!t) return Fail(RT2_ERR_INVALID, "null tracer");
+  if (IsMulti(t)) {
+    if (t->parts.size() != 1) return Fail(RT2_ERR_INVALID, "set_stream: a multi-GPU tracer owns one stream per GPU");
+    return rt2_tracer_set_stream(t->parts[0], s);
+  }
   int rc = Sync(t);
   if (rc != RT2_OK) return rc;
   t->stream = s ? (hipStream_t)s : t->own_stream;
@@ -488,6 +587,7 @@ int rt2_tracer_set_stream(rt2_tracer* t, void* s) {
 
 int rt2_tracer_set_max_depth(rt2_tracer* t, int d) {
   if (!t) return Fail(RT2_ERR_INVALID, "null tracer");
+  RT2_FORWARD(t, rt2_tracer_set_max_depth(p, d));
   // RayTracer::max_depth is a size_t (RayTracer.hpp:32); the kernel keeps it in 16 bits
   if (d > 0xFFFF) return Fail(RT2_ERR_INVALID, "max_depth must be at most 65535");
   int rc = FlushIfChanged(t, t->max_depth, d < 0 ? 0 : d);
@@ -498,6 +598,7 @@ int rt2_tracer_set_max_depth(rt2_tracer* t, int d) {
 
 int rt2_tracer_set_samples_per_pixel(rt2_tracer* t, int spp) {
   if (!t || spp <= 0) return Fail(RT2_ERR_INVALID, "samples_per_pixel must be positive");
+  RT2_FORWARD(t, rt2_tracer_set_samples_per_pixel(p, spp));
   int rc = FlushIfChanged(t, t->camera.SamplesPerPixel(), spp);
   if (rc != RT2_OK) return rc;
   t->camera.SetSamplesPerPixel(spp);
@@ -506,6 +607,7 @@ int rt2_tracer_set_samples_per_pixel(rt2_tracer* t, int spp) {
 
 int rt2_tracer_set_seed(rt2_tracer* t, uint64_t seed) {
   if (!t) return Fail(RT2_ERR_INVALID, "null tracer");
+  RT2_FORWARD(t, rt2_tracer_set_seed(p, seed));
   int rc = FlushIfChanged(t, t->seed, seed);
   if (rc != RT2_OK) return rc;
   t->seed = seed;
@@ -515,6 +617,9 @@ int rt2_tracer_set_seed(rt2_tracer* t, uint64_t seed) {
 int rt2_tracer_set_partition(rt2_tracer* t, int band_h, int rank, int world) {
   if (!t || band_h < 0 || world < 1 || rank < 0 || rank >= world)
     return Fail(RT2_ERR_INVALID, "bad partition (need band_h >= 0, 0 <= rank < world)");
+  if (IsMulti(t)) return Fail(RT2_ERR_INVALID, "set_partition: a multi-GPU tracer partitions itself");
+  if (t->comm && (rank != t->rank || world != t->world || band_h != t->band_h))
+    return Fail(RT2_ERR_INVALID, "set_partition: the tracer is joined to a communicator with another partition");
   t->queued = 0;  // the partition change resets the frame
   int rc = Sync(t);
   if (rc != RT2_OK) return rc;
@@ -527,30 +632,35 @@ int rt2_tracer_set_partition(rt2_tracer* t, int band_h, int rank, int world) {
 
 int rt2_tracer_set_launch_frames(rt2_tracer* t, int n) {
   if (!t || n < 0) return Fail(RT2_ERR_INVALID, "frames_per_launch must be >= 0");
+  RT2_FORWARD(t, rt2_tracer_set_launch_frames(p, n));
   t->launch_frames = n;
   return RT2_OK;
 }
 
 int rt2_tracer_set_work_split(rt2_tracer* t, int items_per_lane) {
   if (!t || items_per_lane < 0) return Fail(RT2_ERR_INVALID, "items_per_lane must be >= 0");
+  RT2_FORWARD(t, rt2_tracer_set_work_split(p, items_per_lane));
   t->work_split = items_per_lane;
   return RT2_OK;
 }
 
 int rt2_tracer_set_batch_max(rt2_tracer* t, int items) {
   if (!t || items < 1) return Fail(RT2_ERR_INVALID, "batch must be >= 1");
+  RT2_FORWARD(t, rt2_tracer_set_batch_max(p, items));
   t->batch_max = items;
   return RT2_OK;
 }
 
 int rt2_tracer_set_sample_budget(rt2_tracer* t, uint64_t bytes) {
   if (!t) return Fail(RT2_ERR_INVALID, "null tracer");
+  RT2_FORWARD(t, rt2_tracer_set_sample_budget(p, bytes));
   t->sample_budget = (size_t)bytes;
   return RT2_OK;
 }
 
 int rt2_tracer_last_launch(const rt2_tracer* t, int* grid, int* chunk_frames, int* variant) {
   if (!t) return Fail(RT2_ERR_INVALID, "null tracer");
+  if (IsMulti(t)) return rt2_tracer_last_launch(t->parts[0], grid, chunk_frames, variant);
   if (grid) *grid = t->last_grid;
   if (chunk_frames) *chunk_frames = t->last_chunk_frames;
   if (variant) *variant = t->last_variant;
@@ -560,6 +670,11 @@ int rt2_tracer_last_launch(const rt2_tracer* t, int* grid, int* chunk_frames, in
 int rt2_tracer_on_resize(rt2_tracer* t, int w, int h) {
   if (!t || w <= 0 || h <= 0) return Fail(RT2_ERR_INVALID, "dims must be positive");
   if (w > 65535 || h > 65535) return Fail(RT2_ERR_INVALID, "dims must be at most 65535");
+  if (IsMulti(t)) {
+    t->width = w;
+    t->height = h;
+    return ForParts(t, [&](rt2_tracer* p) { return rt2_tracer_on_resize(p, w, h); });
+  }
   t->queued = 0;  // OnResize resets the frame
   int rc = Sync(t);
   if (rc != RT2_OK) return rc;
@@ -572,8 +687,44 @@ int rt2_tracer_on_resize(rt2_tracer* t, int w, int h) {
 
 int rt2_tracer_reset(rt2_tracer* t) {
   if (!t) return Fail(RT2_ERR_INVALID, "null tracer");
-  HIP_TRY(hipSetDevice(t->device));
+  RT2_FORWARD(t, rt2_tracer_reset(p));
   return ResetFrame(t);
+}
+
+int rt2_tracer_set_camera(rt2_tracer* t, const rt2_camera_desc* c) {
+  if (!t || !c) return Fail(RT2_ERR_INVALID, "null argument");
+  RT2_FORWARD(t, rt2_tracer_set_camera(p, c));
+  const Camera& cur = t->camera;
+  const vec3 center{c->center[0], c->center[1], c->center[2]};
+  const vec3 look{c->look_at[0], c->look_at[1], c->look_at[2]};
+  const vec3 up{c->view_up[0], c->view_up[1], c->view_up[2]};
+  auto same3 = [](vec3 a, vec3 b) { return memcmp(&a, &b, sizeof(vec3)) == 0; };
+  const bool same = same3(cur.center_, center) && same3(cur.lookat_, look) && same3(cur.view_up_, up) &&
+                    memcmp(&cur.vfov_, &c->vfov, 4) == 0 && memcmp(&cur.defocus_angle_, &c->defocus_angle, 4) == 0 &&
+                    memcmp(&cur.focus_dist_, &c->focus_distance, 4) == 0;
+  if (same) return RT2_OK;  // the reference's lazy camera: nothing dirty, nothing to recompute
+  int rc = Flush(t);        // queued frames render with the camera they were queued under
+  if (rc != RT2_OK) return rc;
+  t->camera.SetCenter(center);
+  t->camera.SetLookAt(look);
+  t->camera.SetViewUp(up);
+  t->camera.SetFOV(c->vfov);
+  t->camera.SetDefocusAngle(c->defocus_angle);
+  t->camera.SetFocusDistance(c->focus_distance);
+  return RT2_OK;
+}
+
+int rt2_tracer_get_camera(const rt2_tracer* t, rt2_camera_desc* o) {
+  if (!t || !o) return Fail(RT2_ERR_INVALID, "null argument");
+  if (IsMulti(t)) return rt2_tracer_get_camera(t->parts[0], o);
+  const Camera& c = t->camera;
+  Put3(o->center, c.center_);
+  Put3(o->look_at, c.lookat_);
+  Put3(o->view_up, c.view_up_);
+  o->vfov = c.vfov_;
+  o->defocus_angle = c.defocus_angle_;
+  o->focus_distance = c.focus_dist_;
+  return RT2_OK;
 }
 
 }  // extern "C"
@@ -726,6 +877,104 @@ int Flush(rt2_tracer* t) {
   return LaunchFrames(t, n);
 }
 
+// ---- multi-GPU gather ----
+// Sizes the root's gathered band stacks and full-image buffers for its current dims and world.
+int EnsureImage(rt2_tracer* root) {
+  const size_t npix = (size_t)root->width * (size_t)root->height;
+  const size_t stacks = (size_t)root->world * (size_t)BandRowsMax(root) * (size_t)root->width * 3 * sizeof(float);
+  if (root->d_image && root->image_pixels == npix && root->stacks_bytes == stacks) return RT2_OK;
+  FreeImage(root);
+  HIP_TRY(hipSetDevice(root->device));
+  HIP_TRY(hipMalloc(&root->d_stacks, std::max<size_t>(stacks, 4)));
+  HIP_TRY(hipMalloc(&root->d_image, std::max<size_t>(npix * 3 * sizeof(float), 4)));
+  HIP_TRY(hipMalloc(&root->d_image_px, std::max<size_t>(npix * 4, 4)));
+  root->stacks_bytes = stacks;
+  root->image_pixels = npix;
+  return RT2_OK;
+}
+
+// Gathers the band stacks of `ranks` (every rank this thread drives: a multi tracer's parts, or
+// one joined tracer) to rank 0 and de-interleaves them there. RCCL unless `loopback` (the ranks
+// share one GPU and their stacks are copied on it). Enqueued on the streams; does not wait.
+int GatherRanks(const std::vector<rt2_tracer*>& ranks, bool loopback) {
+  rt2_tracer* root = nullptr;
+  for (rt2_tracer* p : ranks) {
+    int rc = Flush(p);
+    if (rc != RT2_OK) return rc;
+    if (p->rank == 0) root = p;
+  }
+  const rt2_tracer* r0 = ranks[0];
+  for (rt2_tracer* p : ranks)
+    if (p->width != r0->width || p->height != r0->height || p->frame_idx != r0->frame_idx)
+      return Fail(RT2_ERR_INVALID, "gather: the ranks disagree on dims or frame index");
+  const size_t count = (size_t)BandRowsMax(r0) * (size_t)r0->width * 3;  // floats per rank
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (root) {
+    int rc = EnsureImage(root);
+    if (rc != RT2_OK) return rc;
+    HIP_TRY(hipSetDevice(root->device));
+    e0 = TakeEvent(root);
+    e1 = TakeEvent(root);
+    if (e0) HIP_TRY(hipEventRecord(e0, root->stream));
+  }
+  if (count > 0) {
+    if (loopback) {
+      for (rt2_tracer* p : ranks) {
+        HIP_TRY(hipSetDevice(p->device));
+        if (p != root) {
+          hipEvent_t e = TakeEvent(p);
+          if (!e) return Fail(RT2_ERR_HIP, "event create failed");
+          HIP_TRY(hipEventRecord(e, p->stream));
+          HIP_TRY(hipStreamWaitEvent(root->stream, e, 0));
+          p->event_pool.push_back(e);
+        }
+        HIP_TRY(hipMemcpyAsync(root->d_stacks + (size_t)p->rank * count, p->d_accum, count * sizeof(float),
+                               hipMemcpyDeviceToDevice, root->stream));
+      }
+    } else {
+      for (rt2_tracer* p : ranks)
+        if (!p->comm) return Fail(RT2_ERR_INVALID, "gather: tracer is not part of a communicator");
+      NCCL_TRY(ncclGroupStart());
+      for (rt2_tracer* p : ranks) {
+        ncclResult_t r = ncclGather(p->d_accum, p == root ? root->d_stacks : nullptr, count, ncclFloat32, 0, p->comm,
+                                    p->stream);
+        if (r != ncclSuccess) {
+          (void)ncclGroupEnd();
+          return Fail(RT2_ERR_HIP, std::string("ncclGather: ") + ncclGetErrorString(r));
+        }
+      }
+      NCCL_TRY(ncclGroupEnd());
+    }
+  }
+  if (root) {
+    HIP_TRY(hipSetDevice(root->device));
+    HIP_TRY(LaunchDeinterleave(root->d_stacks, root->d_image, root->d_image_px, root->width, root->height,
+                               BandH(root), root->world, BandRowsMax(root), (int)root->frame_idx, root->stream));
+    if (e1) HIP_TRY(hipEventRecord(e1, root->stream));
+    if (e0 && e1) root->gpending.emplace_back(e0, e1);
+    root->image_frame = root->frame_idx;
+    root->gathers++;
+  }
+  return RT2_OK;
+}
+
+int GatherMulti(rt2_tracer* t) {
+  if (IsMulti(t)) return GatherRanks(t->parts, t->loopback);
+  if (t->comm) return GatherRanks({t}, false);
+  if (t->world > 1) return Fail(RT2_ERR_INVALID, "gather: a partitioned tracer must be joined to a communicator");
+  return GatherRanks({t}, true);  // one GPU, whole image: the "gather" is a device-local copy
+}
+
+// The root tracer holding the gathered image (rank 0), after a gather.
+int ImageRoot(rt2_tracer* t, rt2_tracer** root) {
+  rt2_tracer* r = IsMulti(t) ? t->parts[0] : t;
+  if (r->rank != 0) return Fail(RT2_ERR_INVALID, "the gathered image lives on rank 0");
+  if (r->image_frame < 0) return Fail(RT2_ERR_INVALID, "no gathered image (call rt2_tracer_gather first)");
+  int rc = Sync(r);
+  if (rc != RT2_OK) return rc;
+  *root = r;
+  return RT2_OK;
+}
 }  // namespace
 
 extern "C" {
@@ -738,6 +987,7 @@ extern "C" {
 // of which would be as long as its longest path.
 int rt2_tracer_render(rt2_tracer* t, int n_frames) {
   if (!t || n_frames < 0) return Fail(RT2_ERR_INVALID, "n_frames must be >= 0");
+  RT2_FORWARD(t, rt2_tracer_render(p, n_frames));
   if ((int64_t)t->frame_idx + t->queued + n_frames > 0x7FFFFFFF)
     return Fail(RT2_ERR_INVALID, "frame index overflow");
   if (t->camera.Params().sqrt_spp <= 0) return Fail(RT2_ERR_INVALID, "samples_per_pixel gives sqrt_spp = 0");
@@ -748,6 +998,7 @@ int rt2_tracer_render(rt2_tracer* t, int n_frames) {
 
 int rt2_tracer_set_lazy_frames(rt2_tracer* t, int max_queued) {
   if (!t || max_queued < 0) return Fail(RT2_ERR_INVALID, "max_queued must be >= 0");
+  RT2_FORWARD(t, rt2_tracer_set_lazy_frames(p, max_queued));
   t->lazy_max = max_queued;
   if (max_queued == 0 || t->queued >= max_queued) return Flush(t);
   return RT2_OK;
@@ -757,15 +1008,21 @@ int rt2_tracer_update(rt2_tracer* t) { return rt2_tracer_render(t, 1); }
 
 int rt2_tracer_flush(rt2_tracer* t) {
   if (!t) return Fail(RT2_ERR_INVALID, "null tracer");
+  RT2_FORWARD(t, rt2_tracer_flush(p));
   return Flush(t);
 }
 
 int rt2_tracer_synchronize(rt2_tracer* t) {
   if (!t) return Fail(RT2_ERR_INVALID, "null tracer");
+  RT2_FORWARD(t, rt2_tracer_synchronize(p));
   return Sync(t);
 }
 
-int64_t rt2_tracer_frame_idx(const rt2_tracer* t) { return t ? t->frame_idx + t->queued : -1; }
+int64_t rt2_tracer_frame_idx(const rt2_tracer* t) {
+  if (!t) return -1;
+  if (IsMulti(t)) return rt2_tracer_frame_idx(t->parts[0]);
+  return t->frame_idx + t->queued;
+}
 
 int rt2_tracer_dims(const rt2_tracer* t, int* w, int* h) {
   if (!t) return Fail(RT2_ERR_INVALID, "null tracer");
@@ -774,10 +1031,22 @@ int rt2_tracer_dims(const rt2_tracer* t, int* w, int* h) {
   return RT2_OK;
 }
 
-int rt2_tracer_local_rows(const rt2_tracer* t) { return t ? t->local_rows : -1; }
+int rt2_tracer_local_rows(const rt2_tracer* t) {
+  if (!t) return -1;
+  return IsMulti(t) ? t->height : t->local_rows;
+}
+
+int rt2_tracer_n_gpus(const rt2_tracer* t) {
+  if (!t) return Fail(RT2_ERR_INVALID, "null tracer");
+  return IsMulti(t) ? (int)t->parts.size() : 1;
+}
 
 int rt2_tracer_accumulation(rt2_tracer* t, float* out) {
   if (!t || !out) return Fail(RT2_ERR_INVALID, "null argument");
+  if (IsMulti(t)) {
+    int rc = GatherMulti(t);
+    return rc != RT2_OK ? rc : rt2_tracer_image_accumulation(t, out);
+  }
   int rc = Sync(t);
   if (rc != RT2_OK) return rc;
   size_t n = (size_t)t->width * (size_t)t->local_rows;
@@ -788,14 +1057,18 @@ int rt2_tracer_accumulation(rt2_tracer* t, float* out) {
 int rt2_tracer_non_converted_pixels(rt2_tracer* t, float* out) {
   int rc = rt2_tracer_accumulation(t, out);
   if (rc != RT2_OK) return rc;
-  size_t n = (size_t)t->width * (size_t)t->local_rows * 3;
-  float f = (float)t->frame_idx;  // accumulation / frame_idx_ (RayTracer.cpp:108-109)
+  size_t n = (size_t)t->width * (size_t)rt2_tracer_local_rows(t) * 3;
+  float f = (float)rt2_tracer_frame_idx(t);  // accumulation / frame_idx_ (RayTracer.cpp:108-109)
   for (size_t i = 0; i < n; i++) out[i] = out[i] / f;
   return RT2_OK;
 }
 
 int rt2_tracer_pixels(rt2_tracer* t, uint8_t* out) {
   if (!t || !out) return Fail(RT2_ERR_INVALID, "null argument");
+  if (IsMulti(t)) {
+    int rc = GatherMulti(t);
+    return rc != RT2_OK ? rc : rt2_tracer_image_pixels(t, out);
+  }
   int rc = Sync(t);
   if (rc != RT2_OK) return rc;
   size_t n = (size_t)t->width * (size_t)t->local_rows;
@@ -805,6 +1078,15 @@ int rt2_tracer_pixels(rt2_tracer* t, uint8_t* out) {
 
 int rt2_tracer_pixels_async(rt2_tracer* t, uint8_t* out) {
   if (!t || !out) return Fail(RT2_ERR_INVALID, "null argument");
+  if (IsMulti(t)) {
+    int rc = GatherMulti(t);
+    if (rc != RT2_OK) return rc;
+    rt2_tracer* r = t->parts[0];
+    HIP_TRY(hipSetDevice(r->device));
+    size_t n = (size_t)t->width * (size_t)t->height;
+    if (n) HIP_TRY(hipMemcpyAsync(out, r->d_image_px, n * 4, hipMemcpyDeviceToHost, r->stream));
+    return RT2_OK;
+  }
   int rc = Flush(t);
   if (rc != RT2_OK) return rc;
   HIP_TRY(hipSetDevice(t->device));
@@ -815,6 +1097,15 @@ int rt2_tracer_pixels_async(rt2_tracer* t, uint8_t* out) {
 
 int rt2_tracer_query(rt2_tracer* t) {
   if (!t) return Fail(RT2_ERR_INVALID, "null tracer");
+  if (IsMulti(t)) {
+    int all = 1;
+    for (rt2_tracer* p : t->parts) {
+      int q = rt2_tracer_query(p);
+      if (q < 0) return q;
+      all &= q;
+    }
+    return all;
+  }
   int rc = Flush(t);
   if (rc != RT2_OK) return rc;
   HIP_TRY(hipSetDevice(t->device));
@@ -837,24 +1128,37 @@ void rt2_host_free(void* p) {
 
 int rt2_tracer_copy_accum_device(rt2_tracer* t, void* dst, void* stream) {
   if (!t || !dst) return Fail(RT2_ERR_INVALID, "null argument");
-  int rc = Flush(t);
-  if (rc != RT2_OK) return rc;
-  HIP_TRY(hipSetDevice(t->device));
-  hipStream_t s = stream ? (hipStream_t)stream : t->stream;
-  size_t n = (size_t)t->width * (size_t)t->local_rows;
-  if (s != t->stream) {
-    hipEvent_t e = TakeEvent(t);
-    if (!e) return Fail(RT2_ERR_HIP, "event create failed");
-    HIP_TRY(hipEventRecord(e, t->stream));
-    HIP_TRY(hipStreamWaitEvent(s, e, 0));
-    t->event_pool.push_back(e);
+  const float* src;
+  size_t n;
+  rt2_tracer* o = t;  // the tracer whose stream orders the copy
+  if (IsMulti(t)) {
+    int rc = GatherMulti(t);
+    if (rc != RT2_OK) return rc;
+    o = t->parts[0];
+    src = o->d_image;
+    n = (size_t)t->width * (size_t)t->height;
+  } else {
+    int rc = Flush(t);
+    if (rc != RT2_OK) return rc;
+    src = t->d_accum;
+    n = (size_t)t->width * (size_t)t->local_rows;
   }
-  if (n) HIP_TRY(hipMemcpyAsync(dst, t->d_accum, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s));
+  HIP_TRY(hipSetDevice(o->device));
+  hipStream_t s = stream ? (hipStream_t)stream : o->stream;
+  if (s != o->stream) {
+    hipEvent_t e = TakeEvent(o);
+    if (!e) return Fail(RT2_ERR_HIP, "event create failed");
+    HIP_TRY(hipEventRecord(e, o->stream));
+    HIP_TRY(hipStreamWaitEvent(s, e, 0));
+    o->event_pool.push_back(e);
+  }
+  if (n) HIP_TRY(hipMemcpyAsync(dst, src, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s));
   return RT2_OK;
 }
 
 int rt2_tracer_enable_ray_counts(rt2_tracer* t, int on) {
   if (!t) return Fail(RT2_ERR_INVALID, "null tracer");
+  RT2_FORWARD(t, rt2_tracer_enable_ray_counts(p, on));
   int rc = Sync(t);
   if (rc != RT2_OK) return rc;
   t->ray_counts_on = on != 0;
@@ -864,6 +1168,20 @@ int rt2_tracer_enable_ray_counts(rt2_tracer* t, int on) {
 
 int rt2_tracer_ray_counts(rt2_tracer* t, uint32_t* out) {
   if (!t || !out) return Fail(RT2_ERR_INVALID, "null argument");
+  if (IsMulti(t)) {  // a diagnostic: each GPU's rows read back and placed on the host
+    std::vector<uint32_t> part;
+    for (rt2_tracer* p : t->parts) {
+      part.resize((size_t)p->width * (size_t)p->local_rows);
+      int rc = rt2_tracer_ray_counts(p, part.data());
+      if (rc != RT2_OK) return rc;
+      const int bh = BandH(p);
+      for (int r = 0; r < p->local_rows; r++) {
+        const int y = ((r / bh) * p->world + p->rank) * bh + r % bh;
+        memcpy(out + (size_t)y * p->width, part.data() + (size_t)r * p->width, (size_t)p->width * sizeof(uint32_t));
+      }
+    }
+    return RT2_OK;
+  }
   if (!t->d_ray_counts) return Fail(RT2_ERR_INVALID, "ray counts not enabled");
   int rc = Sync(t);
   if (rc != RT2_OK) return rc;
@@ -874,6 +1192,7 @@ int rt2_tracer_ray_counts(rt2_tracer* t, uint32_t* out) {
 
 int rt2_tracer_enable_stats(rt2_tracer* t, int on) {
   if (!t) return Fail(RT2_ERR_INVALID, "null tracer");
+  RT2_FORWARD(t, rt2_tracer_enable_stats(p, on));
   int rc = FlushIfChanged(t, t->stats_on, on != 0);
   if (rc != RT2_OK) return rc;
   t->stats_on = on != 0;
@@ -882,9 +1201,36 @@ int rt2_tracer_enable_stats(rt2_tracer* t, int on) {
 
 int rt2_tracer_get_stats(rt2_tracer* t, rt2_stats* o) {
   if (!t || !o) return Fail(RT2_ERR_INVALID, "null argument");
+  if (IsMulti(t)) {  // sums over the GPUs; launches per GPU, kernel_ms of the busiest GPU
+    rt2_stats sum;
+    memset(&sum, 0, sizeof(sum));
+    for (rt2_tracer* p : t->parts) {
+      rt2_stats s;
+      int rc = rt2_tracer_get_stats(p, &s);
+      if (rc != RT2_OK) return rc;
+      sum.rays += s.rays;
+      sum.paths += s.paths;
+      sum.bvh_tests += s.bvh_tests;
+      sum.quad_tests += s.quad_tests;
+      sum.sphere_tests += s.sphere_tests;
+      sum.xform_visits += s.xform_visits;
+      sum.medium_tests += s.medium_tests;
+      sum.list_visits += s.list_visits;
+      sum.overflow += s.overflow;
+      sum.launches = std::max(sum.launches, s.launches);
+      sum.kernel_ms = std::max(sum.kernel_ms, s.kernel_ms);
+      for (int k = 0; k < 4; k++) sum.stamps[k] += s.stamps[k];
+      for (int k = 0; k < 8; k++) sum.diag[k] += s.diag[k];
+      sum.gathers += s.gathers;
+      sum.gather_ms += s.gather_ms;
+    }
+    *o = sum;
+    return RT2_OK;
+  }
   int rc = Sync(t);
   if (rc != RT2_OK) return rc;
   unsigned long long s[kStatsSlots];
+  HIP_TRY(hipSetDevice(t->device));
   HIP_TRY(hipMemcpy(s, t->d_stats, sizeof(s), hipMemcpyDeviceToHost));
   o->rays = s[StatsCounters::kRays];
   o->paths = t->paths;  // every (pixel, frame) of a launch finishes exactly one camera path
@@ -899,6 +1245,107 @@ int rt2_tracer_get_stats(rt2_tracer* t, rt2_stats* o) {
   for (int k = 0; k < 8; k++) o->diag[k] = s[StatsCounters::kDiag + k];
   o->launches = t->launches;
   o->kernel_ms = t->kernel_ms;
+  o->gathers = t->gathers;
+  o->gather_ms = t->gather_ms;
+  return RT2_OK;
+}
+
+// ---- multi-GPU entry points ----
+int rt2_tracer_create_multi(const rt2_scene* s, int n, const int* devices, int band_h, rt2_tracer** out) {
+  if (!s || !out) return Fail(RT2_ERR_INVALID, "rt2_tracer_create_multi: null argument");
+  *out = nullptr;
+  if (n < 1 || band_h < 0) return Fail(RT2_ERR_INVALID, "rt2_tracer_create_multi: need n_gpus >= 1, band_h >= 0");
+  std::vector<int> devs((size_t)n);
+  for (int i = 0; i < n; i++) devs[(size_t)i] = devices ? devices[i] : i;
+  const bool all_same = std::all_of(devs.begin(), devs.end(), [&](int d) { return d == devs[0]; });
+  std::vector<int> sorted = devs;
+  std::sort(sorted.begin(), sorted.end());
+  const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
+  if (!distinct && !all_same)
+    return Fail(RT2_ERR_INVALID, "rt2_tracer_create_multi: devices must be distinct (or all one GPU, for tests)");
+  auto m = std::make_unique<rt2_tracer>();
+  m->loopback = n > 1 && all_same;
+  const int bh = band_h > 0 ? band_h : 16;
+  auto cleanup = [&](int rc) {
+    for (rt2_tracer* p : m->parts) rt2_tracer_destroy(p);
+    m->parts.clear();
+    return rc;
+  };
+  for (int i = 0; i < n; i++) {
+    rt2_tracer* p = nullptr;
+    int rc = rt2_tracer_create(s, devs[(size_t)i], &p);
+    if (rc != RT2_OK) return cleanup(rc);
+    m->parts.push_back(p);
+    if ((rc = rt2_tracer_set_partition(p, bh, i, n)) != RT2_OK) return cleanup(rc);
+  }
+  if (!m->loopback) {  // one communicator per device (rank i on devs[i]), RCCL over xGMI
+    std::vector<ncclComm_t> comms((size_t)n, nullptr);
+    ncclResult_t r = ncclCommInitAll(comms.data(), n, devs.data());
+    if (r != ncclSuccess) return cleanup(Fail(RT2_ERR_HIP, std::string("ncclCommInitAll: ") + ncclGetErrorString(r)));
+    for (int i = 0; i < n; i++) m->parts[(size_t)i]->comm = comms[(size_t)i];
+  }
+  m->device = devs[0];
+  m->width = m->parts[0]->width;
+  m->height = m->parts[0]->height;
+  m->band_h = bh;
+  m->world = n;
+  *out = m.release();
+  return RT2_OK;
+}
+
+int rt2_comm_unique_id(uint8_t* out, size_t cap) {
+  if (!out || cap < sizeof(ncclUniqueId)) return Fail(RT2_ERR_INVALID, "rt2_comm_unique_id: need RT2_UNIQUE_ID_BYTES");
+  ncclUniqueId id;
+  NCCL_TRY(ncclGetUniqueId(&id));
+  memcpy(out, &id, sizeof(id));
+  return RT2_OK;
+}
+
+int rt2_tracer_join(rt2_tracer* t, const uint8_t* unique_id, int world, int rank, int band_h) {
+  if (!t || !unique_id) return Fail(RT2_ERR_INVALID, "rt2_tracer_join: null argument");
+  if (IsMulti(t)) return Fail(RT2_ERR_INVALID, "rt2_tracer_join: a multi-GPU tracer has its own communicators");
+  if (t->comm) return Fail(RT2_ERR_INVALID, "rt2_tracer_join: already joined");
+  int rc = rt2_tracer_set_partition(t, band_h > 0 ? band_h : 16, rank, world);
+  if (rc != RT2_OK) return rc;
+  ncclUniqueId id;
+  memcpy(&id, unique_id, sizeof(id));
+  HIP_TRY(hipSetDevice(t->device));
+  NCCL_TRY(ncclCommInitRank(&t->comm, world, id, rank));
+  return RT2_OK;
+}
+
+int rt2_tracer_gather(rt2_tracer* t) {
+  if (!t) return Fail(RT2_ERR_INVALID, "null tracer");
+  return GatherMulti(t);
+}
+
+int rt2_tracer_image_accumulation(rt2_tracer* t, float* out) {
+  if (!t || !out) return Fail(RT2_ERR_INVALID, "null argument");
+  rt2_tracer* r = nullptr;
+  int rc = ImageRoot(t, &r);
+  if (rc != RT2_OK) return rc;
+  size_t n = (size_t)r->width * (size_t)r->height;
+  if (n) HIP_TRY(hipMemcpy(out, r->d_image, n * 3 * sizeof(float), hipMemcpyDeviceToHost));
+  return RT2_OK;
+}
+
+int rt2_tracer_image_non_converted_pixels(rt2_tracer* t, float* out) {
+  int rc = rt2_tracer_image_accumulation(t, out);
+  if (rc != RT2_OK) return rc;
+  rt2_tracer* r = IsMulti(t) ? t->parts[0] : t;
+  size_t n = (size_t)r->width * (size_t)r->height * 3;
+  float f = (float)r->image_frame;  // accumulation / frame_idx_ (RayTracer.cpp:108-109)
+  for (size_t i = 0; i < n; i++) out[i] = out[i] / f;
+  return RT2_OK;
+}
+
+int rt2_tracer_image_pixels(rt2_tracer* t, uint8_t* out) {
+  if (!t || !out) return Fail(RT2_ERR_INVALID, "null argument");
+  rt2_tracer* r = nullptr;
+  int rc = ImageRoot(t, &r);
+  if (rc != RT2_OK) return rc;
+  size_t n = (size_t)r->width * (size_t)r->height;
+  if (n) HIP_TRY(hipMemcpy(out, r->d_image_px, n * 4, hipMemcpyDeviceToHost));
   return RT2_OK;
 }
 
@@ -923,12 +1370,16 @@ int rt2_selftest(int device, int which, uint64_t n, uint64_t seed, uint64_t* mis
 
 int rt2_tracer_reset_stats(rt2_tracer* t) {
   if (!t) return Fail(RT2_ERR_INVALID, "null tracer");
+  RT2_FORWARD(t, rt2_tracer_reset_stats(p));
   int rc = Sync(t);
   if (rc != RT2_OK) return rc;
+  HIP_TRY(hipSetDevice(t->device));
   HIP_TRY(hipMemset(t->d_stats, 0, kStatsSlots * sizeof(unsigned long long)));
   t->launches = 0;
   t->paths = 0;
   t->kernel_ms = 0;
+  t->gathers = 0;
+  t->gather_ms = 0;
   return RT2_OK;
 }
 

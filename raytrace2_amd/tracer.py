@@ -17,7 +17,7 @@ from typing import List, Optional, Sequence, Tuple
 import numpy as np
 
 from ._native import AppSettings as _AppSettings
-from ._native import CameraDesc, SceneInfo, Stats, check, lib
+from ._native import UNIQUE_ID_BYTES, CameraDesc, SceneInfo, Stats, check, lib
 
 DEFAULT_SEED = 0x5EED2024
 
@@ -183,20 +183,41 @@ def assemble_bands(parts: Sequence[np.ndarray], height: int, band_h: int) -> np.
     return out
 
 
+def comm_unique_id() -> bytes:
+    """rt2_comm_unique_id: the RCCL id rank 0 makes and the caller broadcasts before join()."""
+    buf = (ctypes.c_uint8 * UNIQUE_ID_BYTES)()
+    check(lib.rt2_comm_unique_id(buf, UNIQUE_ID_BYTES))
+    return bytes(buf)
+
+
 class RayTracer:
-    """cpu::RayTracer (RayTracer.hpp:15-42) on one MI355X GPU.
+    """cpu::RayTracer (RayTracer.hpp:15-42) on one or more MI355X GPUs.
 
     Update() renders one frame (one sample per pixel) exactly like RayTracer::Update; Render(n) is
     n Update() calls in one kernel launch. Image buffers hold this tracer's local rows (all rows
-    unless set_partition() was called).
+    unless set_partition()/join() was called). With `n_gpus` or `devices` the tracer renders on
+    several GPUs of this process (rt2_tracer_create_multi: interleaved row bands, RCCL gather) and
+    its readbacks return the full image.
+
+    `camera`, like the reference's borrowed `Camera* camera` (RayTracer.hpp:31), is read at every
+    Update()/Render() when set: a moved camera applies from the next frame (RayTracer.cpp:56).
     """
 
-    def __init__(self, scene: Scene, device: int = 0):
+    def __init__(self, scene: Scene, device: int = 0, *, n_gpus: Optional[int] = None,
+                 devices: Optional[Sequence[int]] = None, band_h: int = 0):
         h = ctypes.c_void_p()
-        check(lib.rt2_tracer_create(scene._h, device, ctypes.byref(h)))
+        if n_gpus is None and devices is None:
+            check(lib.rt2_tracer_create(scene._h, device, ctypes.byref(h)))
+            self.devices = [device]
+        else:
+            devs = list(devices) if devices is not None else list(range(device, device + int(n_gpus)))
+            arr = (ctypes.c_int * len(devs))(*devs)
+            check(lib.rt2_tracer_create_multi(scene._h, len(devs), arr, int(band_h), ctypes.byref(h)))
+            self.devices = devs
         self._h = h
-        self.device = device
+        self.device = self.devices[0]
         self._max_depth = 50
+        self.camera: Optional[Camera] = None
 
     def close(self):
         if getattr(self, "_h", None) and self._h.value:
@@ -226,10 +247,16 @@ class RayTracer:
     def Reset(self) -> None:
         check(lib.rt2_tracer_reset(self._h))
 
+    def _push_camera(self) -> None:
+        if self.camera is not None:
+            self.set_camera(self.camera)
+
     def Update(self, scene: Optional[Scene] = None) -> None:
+        self._push_camera()  # camera->Update() (RayTracer.cpp:56)
         check(lib.rt2_tracer_update(self._h))
 
     def Render(self, n_frames: int) -> None:
+        self._push_camera()
         check(lib.rt2_tracer_render(self._h, int(n_frames)))
 
     def FrameIdx(self) -> int:
@@ -262,6 +289,47 @@ class RayTracer:
         return out
 
     # -- MI355X extensions ------------------------------------------------------------------
+    def set_camera(self, cam: Camera) -> None:
+        """rt2_tracer_set_camera: the camera's setter fields for the next frames (queued frames
+        keep the camera they were queued under; the accumulation is not reset)."""
+        d = cam._desc()
+        check(lib.rt2_tracer_set_camera(self._h, ctypes.byref(d)))
+
+    def get_camera(self) -> Camera:
+        d = CameraDesc()
+        check(lib.rt2_tracer_get_camera(self._h, ctypes.byref(d)))
+        return Camera._from_desc(d)
+
+    def n_gpus(self) -> int:
+        return int(check(lib.rt2_tracer_n_gpus(self._h)))
+
+    def join(self, unique_id: bytes, world: int, rank: int, band_h: int = 16) -> None:
+        """rt2_tracer_join: partition (band_h, rank, world) + this rank of an RCCL communicator."""
+        buf = (ctypes.c_uint8 * UNIQUE_ID_BYTES).from_buffer_copy(unique_id[:UNIQUE_ID_BYTES])
+        check(lib.rt2_tracer_join(self._h, buf, int(world), int(rank), int(band_h)))
+
+    def gather(self) -> None:
+        """rt2_tracer_gather: collective; the full image lands on rank 0 (enqueued, no wait)."""
+        check(lib.rt2_tracer_gather(self._h))
+
+    def image_accumulation(self) -> np.ndarray:
+        w, h = self.Dims()
+        out = np.zeros((h, w, 3), np.float32)
+        check(lib.rt2_tracer_image_accumulation(self._h, _fp(out)))
+        return out
+
+    def image_non_converted_pixels(self) -> np.ndarray:
+        w, h = self.Dims()
+        out = np.zeros((h, w, 3), np.float32)
+        check(lib.rt2_tracer_image_non_converted_pixels(self._h, _fp(out)))
+        return out
+
+    def image_pixels(self) -> np.ndarray:
+        w, h = self.Dims()
+        out = np.zeros((h, w, 4), np.uint8)
+        check(lib.rt2_tracer_image_pixels(self._h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))))
+        return out
+
     def set_seed(self, seed: int) -> None:
         check(lib.rt2_tracer_set_seed(self._h, int(seed)))
 

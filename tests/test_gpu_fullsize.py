@@ -1,0 +1,100 @@
+"""Bit-exact parity at the BASELINE configs' full geometry and sample settings, including the
+stratum wrap: the reference's frame f uses stratum (f % sq, f / sq % sq) (RayTracer.cpp:59-60), so
+frames past sq^2 revisit the strata — the headline's frames 961-999 (spp 1000, sq 31), book 1's
+484-499 (sq 22) and Cornell volume's 3969+ (sq 63).
+
+Where the oracle would take minutes for a whole image it renders a band subset of rows (the GPU
+renders the same partition), and where a late frame range matters it continues from the GPU's own
+accumulation at frame k: the accumulation is a frame-ordered running sum (RayTracer.cpp:64), so
+oracle(frames k..n | start = GPU(frames 0..k)) must equal GPU(frames 0..n) bit for bit.
+"""
+import numpy as np
+import pytest
+
+from conftest import scene_path
+from helpers import SEED, gpu_render, oracle_render
+
+pytestmark = pytest.mark.gpu
+
+THREADS = 16  # the GPU box's CPU share
+
+
+def _same(a, b):
+    return np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+def _check(name, w, h, spp, frames, **kw):
+    part = {k: v for k, v in kw.items() if k in ("band_h", "rank", "world")}
+    acc, rc, st, _ = gpu_render(name, w, h, spp, frames, **kw)
+    o_acc, o_rc, o_cnt = oracle_render(name, w, h, spp, frames, forward=True, threads=THREADS, **part)
+    assert st["overflow"] == 0
+    np.testing.assert_array_equal(rc, o_rc)
+    assert st["rays"] == o_cnt["rays"]
+    mism = np.count_nonzero(acc.view(np.uint32) != o_acc.view(np.uint32))
+    assert mism == 0, f"{mism} of {acc.size} floats differ"
+    return acc, rc
+
+
+def _check_continuation(name, w, h, spp, k, n, **part):
+    """GPU frames 0..n vs oracle frames k..n started from the GPU's accumulation at frame k."""
+    from oracle.oracle import OracleScene
+    a_k, rc_k, _, _ = gpu_render(name, w, h, spp, k, **part)
+    a_n, rc_n, _, _ = gpu_render(name, w, h, spp, n, **part)
+    o = OracleScene(scene_path(name), SEED)
+    o_acc = a_k.copy()
+    o_rc = np.zeros_like(rc_k)
+    o.render(w, h, spp, n - k, frame_begin=k, accum=o_acc, ray_counts=o_rc, forward=True, threads=THREADS, **part)
+    np.testing.assert_array_equal(rc_n - rc_k, o_rc)
+    assert _same(a_n, o_acc)
+
+
+def test_c1_cornell_400_at_64spp_full_image():
+    """BASELINE configs[0]: cornell_box_original.json 400x400 @ 64 spp, the whole image."""
+    _check("cornell_box_original", 400, 400, 64, 64)
+
+
+def test_c2_cornell_1024_all_1000_frames_band():
+    """BASELINE configs[1] (the headline): 1024^2, spp 1000, every frame 0..999 (strata wrap at
+    961), on rank 5 of a 32-way 16-row band split (32 rows x 1024)."""
+    _check("cornell_box_original", 1024, 1024, 1000, 1000, band_h=16, rank=5, world=32)
+
+
+def test_c3_book1_full_width_band_all_500_frames():
+    """BASELINE configs[2]: book 1 at 1920x1080, spp 500 (sq 22: frames 484-499 wrap), a full-width
+    band of 8 rows (rank 67 of 135)."""
+    _check("final_render_book_1", 1920, 1080, 500, 500, band_h=8, rank=67, world=135)
+
+
+def test_c4_cornell_volume_spp4000_first_frames():
+    """BASELINE configs[3]: Cornell volume 1024^2 at spp 4000 (sq 63), 64 frames on 16 rows."""
+    _check("cornell_box_volume", 1024, 1024, 4000, 64, band_h=16, rank=17, world=64)
+
+
+def test_c4_cornell_volume_spp4000_across_sq2():
+    """Frames 3950..3999 of spp 4000 cross sq^2 = 3969 (stratum (0, 0) again at 3969)."""
+    _check_continuation("cornell_box_volume", 1024, 1024, 4000, 3950, 4000, band_h=8, rank=40, world=128)
+
+
+def test_c5_book2_full_width_band():
+    """BASELINE configs[4]: book 2 at 800x800, spp 10000 (sq 100), 24 frames on an 8-row band."""
+    _check("book2_final_scene_10000_samples", 800, 800, 10000, 24, band_h=8, rank=50, world=100)
+
+
+def test_c2_headline_last_frames_full_width():
+    """The headline's wrap region on a wider band: frames 950..999 continued from the GPU."""
+    _check_continuation("cornell_box_original", 1024, 1024, 1000, 950, 1000, band_h=64, rank=7, world=16)
+
+
+@pytest.mark.parametrize("split", [0, 1, 3, 64])
+def test_spp20_sq2_below_spp_frames_wrap(split):
+    """spp 20: sq = 4, sq^2 = 16 < spp, so frames 16..19 (and 20..39) wrap; chunks of a split
+    launch start mid-cycle."""
+    acc, rc = _check("cornell_box_original", 72, 40, 20, 40, work_split=split)
+    if split:
+        acc0, _, _, _ = gpu_render("cornell_box_original", 72, 40, 20, 40, work_split=0)
+        assert _same(acc, acc0)
+
+
+def test_frames_beyond_sq2_in_several_launches():
+    """spp 16 (sq 4), 40 frames as launches of 7 frames: launch boundaries inside the cycle."""
+    _check("cornell_box_volume", 64, 48, 16, 40, launch_frames=7)

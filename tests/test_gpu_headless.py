@@ -42,6 +42,16 @@ def test_headless_app_matches_python_mirror(have_gpu, tmp_path, name):
     assert open(a, "rb").read() == open(b, "rb").read()
 
 
+def test_headless_app_multi_gpu_path(have_gpu, tmp_path):
+    """rt2::RayTracer(scene, 0, n_gpus) over rt2_tracer_create_multi (RCCL, one GPU on the test box):
+    the same PNG as the one-GPU path."""
+    a, b = str(tmp_path / "multi.png"), str(tmp_path / "one.png")
+    out = _run([scene_path("cornell_box_original"), a, "--samples", "12", "--size", "80x72", "--gpus", "1"])
+    assert out["gpus"] == 1 and out["frames"] == 12
+    _run([scene_path("cornell_box_original"), b, "--samples", "12", "--size", "80x72"])
+    assert open(a, "rb").read() == open(b, "rb").read()
+
+
 def test_headless_app_reads_settings(have_gpu, tmp_path):
     st = tmp_path / "settings.json"
     st.write_text(json.dumps({"render_once": True, "save_after_render_once": True, "num_samples": 9,

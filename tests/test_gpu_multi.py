@@ -1,0 +1,191 @@
+"""Multi-GPU path through the C ABI and the tracer-level camera (RayTracer.hpp:31).
+
+On the one-GPU test box:
+  * rt2_tracer_create_multi with one device runs the real RCCL path (ncclCommInitAll with a
+    communicator of size 1, ncclGather, de-interleave kernel) and must equal the plain render;
+  * a device listed n times runs n row-band partitions on one GPU with device-local copies in
+    place of RCCL: the partition, padding, de-interleave and Pixels() logic of an n-GPU job;
+  * rt2_tracer_join with world 1 runs the one-process-per-GPU path (ncclCommInitRank).
+The multi-process RCCL path at N > 1 is exercised by bench.py under torch.distributed.run; its
+partition/gather glue is covered on CPU by tests/test_dist.py.
+"""
+import numpy as np
+import pytest
+
+from conftest import scene_path
+from helpers import SEED
+
+pytestmark = pytest.mark.gpu
+
+
+def _plain(name, w, h, spp, frames, counts=True):
+    import raytrace2_amd as R
+    sc = R.Scene(scene_path(name), SEED)
+    tr = R.RayTracer(sc, 0)
+    tr.set_seed(SEED)
+    tr.SetSamplesPerPixel(spp)
+    if counts:
+        tr.enable_ray_counts(True)
+    tr.OnResize((w, h))
+    tr.Render(frames)
+    out = tr.Accumulation(), tr.Pixels(), (tr.ray_counts() if counts else None), tr.stats()
+    tr.close()
+    return out
+
+
+def _multi(name, w, h, spp, frames, *, devices, band_h=8, counts=True, updates=False):
+    import raytrace2_amd as R
+    sc = R.Scene(scene_path(name), SEED)
+    tr = R.RayTracer(sc, devices=devices, band_h=band_h)
+    assert tr.n_gpus() == len(devices)
+    tr.set_seed(SEED)
+    tr.SetSamplesPerPixel(spp)
+    if counts:
+        tr.enable_ray_counts(True)
+    tr.OnResize((w, h))
+    assert tr.local_rows() == h
+    if updates:
+        for _ in range(frames):
+            tr.Update(sc)
+    else:
+        tr.Render(frames)
+    acc, px = tr.Accumulation(), tr.Pixels()
+    rc = tr.ray_counts() if counts else None
+    st = tr.stats()
+    ncp = tr.NonConvertedPixels()
+    assert tr.FrameIdx() == frames
+    tr.close()
+    return acc, px, rc, st, ncp
+
+
+def _same(a, b):
+    return np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+def test_one_gpu_through_rccl_is_bit_identical():
+    """A communicator of size 1: ncclGather + de-interleave reproduce the plain render bit for bit."""
+    w, h, spp, frames = 61, 47, 16, 6
+    acc, px, rc, st = _plain("cornell_box_volume", w, h, spp, frames)
+    macc, mpx, mrc, mst, ncp = _multi("cornell_box_volume", w, h, spp, frames, devices=[0], band_h=16)
+    assert _same(macc, acc) and np.array_equal(mpx, px) and np.array_equal(mrc, rc)
+    assert mst["rays"] == st["rays"] and mst["gathers"] >= 1 and mst["gather_ms"] > 0
+    assert _same(ncp, acc / np.float32(frames))
+
+
+@pytest.mark.parametrize("n,band_h", [(2, 8), (3, 8), (8, 4), (8, 16)])
+def test_partitions_on_one_gpu_reassemble(n, band_h):
+    """n row-band partitions (uneven: 45 rows) gathered and de-interleaved equal one render."""
+    w, h, spp, frames = 50, 45, 16, 5
+    acc, px, rc, st = _plain("cornell_box_original", w, h, spp, frames)
+    macc, mpx, mrc, mst, _ = _multi("cornell_box_original", w, h, spp, frames, devices=[0] * n, band_h=band_h,
+                                    updates=(n == 3))
+    assert _same(macc, acc)
+    assert np.array_equal(mpx, px)
+    assert np.array_equal(mrc, rc)
+    assert mst["rays"] == st["rays"] and mst["paths"] == st["paths"]
+
+
+def test_more_partitions_than_bands():
+    """Ranks that own no rows still take part in the gather (padded, equal send counts)."""
+    w, h = 33, 10
+    acc, px, rc, _ = _plain("cornell_box_original", w, h, 16, 3)
+    macc, mpx, mrc, _, _ = _multi("cornell_box_original", w, h, 16, 3, devices=[0] * 4, band_h=8)
+    assert _same(macc, acc) and np.array_equal(mpx, px) and np.array_equal(mrc, rc)
+
+
+def test_multi_reset_resize_and_explicit_gather():
+    import raytrace2_amd as R
+    sc = R.Scene(scene_path("cornell_box_original"), SEED)
+    tr = R.RayTracer(sc, devices=[0, 0], band_h=8)
+    tr.set_seed(SEED)
+    tr.SetSamplesPerPixel(16)
+    tr.OnResize((20, 30))
+    tr.Render(4)
+    tr.Reset()
+    tr.OnResize((40, 24))
+    tr.Render(3)
+    tr.gather()
+    img = tr.image_accumulation()
+    assert img.shape == (24, 40, 3)
+    acc, px, _, _ = _plain("cornell_box_original", 40, 24, 16, 3, counts=False)
+    assert _same(img, acc) and np.array_equal(tr.image_pixels(), px)
+    with pytest.raises(R.Rt2Error):
+        tr.set_partition(8, 0, 2)  # a multi tracer partitions itself
+    tr.close()
+
+
+def test_join_world_one():
+    """The one-process-per-GPU path (rt2_comm_unique_id + rt2_tracer_join = ncclCommInitRank)."""
+    import raytrace2_amd as R
+    w, h, spp, frames = 48, 40, 16, 4
+    acc, px, _, _ = _plain("cornell_box_original", w, h, spp, frames, counts=False)
+    sc = R.Scene(scene_path("cornell_box_original"), SEED)
+    tr = R.RayTracer(sc, 0)
+    tr.set_seed(SEED)
+    tr.SetSamplesPerPixel(spp)
+    tr.OnResize((w, h))
+    tr.join(R.comm_unique_id(), 1, 0, 16)
+    tr.Render(frames)
+    with pytest.raises(R.Rt2Error):
+        tr.image_accumulation()  # nothing gathered yet
+    tr.gather()
+    assert _same(tr.image_accumulation(), acc)
+    assert np.array_equal(tr.image_pixels(), px)
+    assert _same(tr.image_non_converted_pixels(), acc / np.float32(frames))
+    tr.close()
+
+
+def test_camera_moved_between_updates_matches_oracle():
+    """The reference re-reads its borrowed camera at every Update (RayTracer.cpp:56): frames render
+    with the camera current when they were queued; the accumulation is not reset."""
+    import raytrace2_amd as R
+    from oracle.oracle import OracleScene
+    name, w, h, spp = "cornell_box_original", 40, 36, 16
+    sc = R.Scene(scene_path(name), SEED)
+    cam_a = sc.cam
+    cam_b = R.Camera((250.0, 300.0, -760.0), (278.0, 270.0, 0.0), (0.0, 1.0, 0.0), 44.0, 0.0, 1.0)
+    cam_c = R.Camera((300.0, 250.0, -820.0), (270.0, 290.0, 10.0), (0.1, 1.0, 0.0), 36.0, 1.5, 800.0)
+    schedule = [(cam_a, 3), (cam_b, 4), (cam_c, 2), (cam_a, 1)]
+
+    tr = R.RayTracer(sc, 0)
+    tr.set_seed(SEED)
+    tr.SetSamplesPerPixel(spp)
+    tr.enable_ray_counts(True)
+    tr.OnResize((w, h))
+    for cam, n in schedule:
+        tr.camera = cam  # like moving scene.cam under the borrowed pointer
+        for _ in range(n):
+            tr.Update(sc)  # queued: the camera change flushes the frames queued before it
+    acc, rc = tr.Accumulation(), tr.ray_counts()
+    assert tr.get_camera() == cam_a
+    tr.close()
+
+    o = OracleScene(scene_path(name), SEED)
+    o_acc = np.zeros((h, w, 3), np.float32)
+    o_rc = np.zeros((h, w), np.uint32)
+    f = 0
+    for cam, n in schedule:
+        o.set_camera(cam.center, cam.look_at, cam.view_up, cam.vfov, cam.defocus_angle, cam.focus_distance)
+        o.render(w, h, spp, n, frame_begin=f, accum=o_acc, ray_counts=o_rc, forward=True)
+        f += n
+    np.testing.assert_array_equal(rc, o_rc)
+    assert _same(acc, o_acc)
+
+
+def test_camera_setter_on_multi_tracer():
+    import raytrace2_amd as R
+    sc = R.Scene(scene_path("cornell_box_original"), SEED)
+    cam_b = R.Camera((250.0, 300.0, -760.0), (278.0, 270.0, 0.0), (0.0, 1.0, 0.0), 44.0, 0.0, 1.0)
+    outs = []
+    for devs in (None, [0, 0, 0]):
+        tr = R.RayTracer(sc, 0) if devs is None else R.RayTracer(sc, devices=devs, band_h=8)
+        tr.set_seed(SEED)
+        tr.SetSamplesPerPixel(16)
+        tr.OnResize((30, 30))
+        tr.Render(2)
+        tr.set_camera(cam_b)
+        tr.Render(2)
+        outs.append(tr.Accumulation())
+        assert tr.get_camera() == cam_b
+        tr.close()
+    assert _same(outs[0], outs[1])
