@@ -306,6 +306,7 @@ def main():
         per_rank.append({"rank": er, "rows": tr.local_rows(), "elapsed_s": el, "rays": st["rays"],
                          "kernel_ms": st["kernel_ms"], "launches": st["launches"], "gather_ms": st["gather_ms"],
                          "gathers": st["gathers"], "mray_s": st["rays"] / el / 1e6})
+    launch_shape = tr.last_launch()  # the timed launches' shape (before the stats pass below)
     me = per_rank[-1] if mode != "emulate" else max(per_rank, key=lambda r: r["elapsed_s"])
     if mode == "ranks":
         gathered = [None] * world
@@ -370,7 +371,7 @@ def main():
                     f"{a.seed:#x}",
             "config": {"workload": workload, "parallelism": par, "partition": partition,
                        "launch_frames": a.spp * a.steps // max(1, me["launches"]),
-                       "work_split": tr.last_launch()},
+                       "work_split": launch_shape},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "detail": {"rays": int(rays_total), "launches": me["launches"], "setup_s": round(setup_s, 3),

@@ -108,11 +108,13 @@ RT2_API int rt2_tracer_set_samples_per_pixel(rt2_tracer* tr, int spp); /* App.cp
 RT2_API int rt2_tracer_set_seed(rt2_tracer* tr, uint64_t seed);
 RT2_API int rt2_tracer_set_partition(rt2_tracer* tr, int band_h, int rank, int world);
 RT2_API int rt2_tracer_set_launch_frames(rt2_tracer* tr, int frames_per_launch); /* 0 = all */
-/* Work split: each pixel's frames of a launch are cut into chunks so that the launch holds about
- * `items_per_lane` work items (pixel x frame chunk) per resident GPU lane (default 64; 0 = one chunk
- * per pixel). Every frame's sample goes to a per-frame buffer and is summed in frame order after
- * the launch, so results do not depend on the split. The buffer is bounded by `bytes` (default
- * 16 GiB): a render needing more runs as several launches. */
+/* Work split: a launch's frames are cut into chunks and every (pixel, chunk) is one work item. A
+ * chunk starting with R frames left holds about R * pixels / (k * resident GPU lanes) frames, k =
+ * `items_per_lane` (default 16), at least 1 and at most 64 (RT2_CHUNK_MAX): long items early, short
+ * ones at the end of the launch. 0 = one chunk (each pixel's frames in one item). Every frame's
+ * sample goes to a per-frame buffer and is summed in frame order after the launch, so results do
+ * not depend on the split. The buffer is bounded by `bytes` (default 16 GiB): a render needing
+ * more runs as several launches. */
 RT2_API int rt2_tracer_set_lazy_frames(rt2_tracer* tr, int max_queued);
 RT2_API int rt2_tracer_flush(rt2_tracer* tr); /* launch the queued frames now (does not wait) */
 RT2_API int rt2_tracer_set_work_split(rt2_tracer* tr, int items_per_lane);
@@ -120,7 +122,7 @@ RT2_API int rt2_tracer_set_sample_budget(rt2_tracer* tr, uint64_t bytes);
 /* Most work items a GPU wave reserves with one atomic (default 64); batches shrink as the launch
  * drains. */
 RT2_API int rt2_tracer_set_batch_max(rt2_tracer* tr, int items);
-/* Launch shape of the last render: persistent workgroups, frames per work item, kernel variant. */
+/* Launch shape of the last render: persistent workgroups, frames of its first chunk, kernel variant. */
 RT2_API int rt2_tracer_last_launch(const rt2_tracer* tr, int* grid, int* chunk_frames, int* variant);
 RT2_API int rt2_tracer_on_resize(rt2_tracer* tr, int width, int height);
 RT2_API int rt2_tracer_reset(rt2_tracer* tr);

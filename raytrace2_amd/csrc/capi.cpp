@@ -89,7 +89,13 @@ struct rt2_tracer {
   float* d_samples = nullptr;
   size_t samples_bytes = 0;
   size_t sample_budget = size_t(16) << 30;  // bytes; bounds the frames per launch
-  int work_split = 64;                     // target work items per resident lane (0: one chunk)
+  int work_split = 16;                     // chunk schedule: work left split into >= k items per lane (0: one chunk)
+  int chunk_max = 64;                      // longest chunk (frames)
+  uint32_t* d_chunks = nullptr;            // chunk table of the last launch shape (ChunkSchedule)
+  size_t chunks_bytes = 0;
+  uint32_t n_chunks = 0;
+  int first_chunk_frames = 0;
+  uint64_t chunk_key[6] = {~0ull, 0, 0, 0, 0, 0};
   int batch_max = 64;                      // most work items a wave reserves with one atomic
   int last_chunk_frames = 0;
   int occ_key = -1, occ_blocks = 1;  // cached occupancy of the last kernel instantiation
@@ -501,6 +507,7 @@ int rt2_tracer_create(const rt2_scene* s, int device, rt2_tracer** out) {
   if (const char* e = getenv("RT2_NO_HYBRID")) t->use_hybrid = e[0] == '0';
   if (const char* e = getenv("RT2_FORCE_HYBRID")) t->force_hybrid = e[0] == '1';
   if (const char* e = getenv("RT2_HYBRID_RECORDS")) t->hybrid_cap = atoi(e);
+  if (const char* e = getenv("RT2_CHUNK_MAX")) t->chunk_max = std::max(1, atoi(e));
   // App.cpp:122-125,157: scene dims when present, else the window default 1600x900
   int w = s->scene.dims_x > 0 && s->scene.dims_y > 0 ? s->scene.dims_x : 1600;
   int h = s->scene.dims_x > 0 && s->scene.dims_y > 0 ? s->scene.dims_y : 900;
@@ -545,6 +552,7 @@ void rt2_tracer_destroy(rt2_tracer* t) {
   (void)hipFree(t->d_lind);
   (void)hipFree(t->d_work);
   (void)hipFree(t->d_stats);
+  (void)hipFree(t->d_chunks);
   if (t->own_stream) (void)hipStreamDestroy(t->own_stream);
   delete t;
 }
@@ -730,6 +738,62 @@ int rt2_tracer_get_camera(const rt2_tracer* t, rt2_camera_desc* o) {
 }  // extern "C"
 
 namespace {
+Magic MakeMagic(uint32_t d) {  // rt2_layout.h Magic: floor(n / d) for n < 2^31
+  uint32_t l = 0;
+  while ((1ull << l) < (uint64_t)d) l++;
+  const uint64_t m = ((1ull << (31 + l)) + d - 1) / d;
+  return Magic{(uint32_t)m, 31 + l};
+}
+
+// Frame chunks of one launch: frames [fb, fb + n) cut into chunks, every pixel's chunk c one work
+// item (chunk-major). A chunk starting with R frames left holds about R * T / (k * L) frames (T =
+// items per chunk, L = resident lanes, k = work_split), at least 1 and at most chunk_max: early
+// items are long (few item setups per sample) and the last ones short, so the launch's tail — the
+// time in which lanes run out of work while others finish their item — stays short. k = 0: one
+// chunk (each pixel's frames in one item). Cached: the bench repeats one launch shape.
+int ChunkSchedule(rt2_tracer* t, int fb, int n, uint32_t tile_items, int64_t lanes, int sq) {
+  const uint64_t key[6] = {(uint64_t)fb, (uint64_t)n, tile_items, (uint64_t)lanes,
+                           (uint64_t)t->work_split | ((uint64_t)t->chunk_max << 32), (uint64_t)sq};
+  if (t->d_chunks && memcmp(key, t->chunk_key, sizeof(key)) == 0) return RT2_OK;
+  // items must stay below 2^31 (kernel index arithmetic): shortest chunk that allows it
+  const int64_t max_chunks = std::max<int64_t>(1, (int64_t)0x7FFFFFFF / tile_items);
+  const int lo = (int)std::max<int64_t>(1, ((int64_t)n + max_chunks - 1) / max_chunks);
+  std::vector<uint32_t> tab;
+  int first = 0;
+  for (int s = 0; s < n;) {
+    int len = n - s;
+    if (t->work_split > 0) {
+      const double want = (double)(n - s) * (double)tile_items / ((double)t->work_split * (double)lanes);
+      len = (int)std::min<double>(want, (double)t->chunk_max);
+    }
+    len = std::max(len, lo);
+    len = std::min({len, n - s, 0x10000});  // the kernel keeps a chunk's frames left in 16 bits
+    const uint32_t f = (uint32_t)(fb + s), usq = (uint32_t)sq;
+    tab.push_back(f);
+    tab.push_back((f % usq) | (((f / usq) % usq) << 16));  // RayTracer.cpp:59-60
+    if (s == 0) first = len;
+    s += len;
+  }
+  tab.push_back((uint32_t)(fb + n));
+  tab.push_back(0u);
+  const size_t bytes = tab.size() * sizeof(uint32_t);
+  if (bytes > t->chunks_bytes) {
+    HIP_TRY(hipStreamSynchronize(t->stream));  // the old table may still be read
+    (void)hipFree(t->d_chunks);
+    t->d_chunks = nullptr;
+    t->chunks_bytes = 0;
+    HIP_TRY(hipMalloc(&t->d_chunks, bytes));
+    t->chunks_bytes = bytes;
+  } else if (t->d_chunks) {
+    HIP_TRY(hipStreamSynchronize(t->stream));
+  }
+  HIP_TRY(hipMemcpy(t->d_chunks, tab.data(), bytes, hipMemcpyHostToDevice));
+  t->n_chunks = (uint32_t)(tab.size() / 2 - 1);
+  t->first_chunk_frames = first;
+  memcpy(t->chunk_key, key, sizeof(key));
+  return RT2_OK;
+}
+
 // Launches frames [frame_idx, frame_idx + n_frames) now.
 int LaunchFrames(rt2_tracer* t, int n_frames) {
   if (n_frames == 0 || t->local_rows == 0) {
@@ -756,6 +820,10 @@ int LaunchFrames(rt2_tracer* t, int n_frames) {
   p.world = t->world;
   p.tiles_x = (t->width + 7) / 8;
   p.tile_items = (uint32_t)p.tiles_x * (uint32_t)((t->local_rows + 7) / 8) * 64u;
+  p.div_tile_items = MakeMagic(p.tile_items);
+  p.div_tiles_x = MakeMagic((uint32_t)p.tiles_x);
+  p.div_band_h = MakeMagic((uint32_t)p.band_h);
+  p.div_band_w = MakeMagic((uint32_t)p.band_h * (uint32_t)p.world);
   p.local_pixels = (uint32_t)t->width * (uint32_t)t->local_rows;
   p.max_depth = t->max_depth;
   p.seed_lo = (uint32_t)t->seed;
@@ -839,21 +907,17 @@ int LaunchFrames(rt2_tracer* t, int n_frames) {
     // resident lane: a persistent lane's last item is then short, and a small partition (a row
     // band of an 8-GPU split) still fills every CU. Samples land in the per-frame buffer, so the
     // accumulation order does not depend on the split.
-    int64_t chunks = 1;
-    if (t->work_split > 0)
-      chunks = std::max<int64_t>(1, ((int64_t)t->work_split * resident + p.tile_items - 1) / p.tile_items);
-    chunks = std::min<int64_t>(chunks, std::max<int64_t>(1, (int64_t)0x7FFFFFFF / p.tile_items));
-    chunks = std::min<int64_t>(chunks, p.n_frames);
-    chunks = std::max<int64_t>(chunks, ((int64_t)p.n_frames + 0xFFFF) / 0x10000);  // kernel: <= 2^16 frames per item
-    p.chunk_frames = (int)((p.n_frames + chunks - 1) / chunks);
-    chunks = (p.n_frames + p.chunk_frames - 1) / p.chunk_frames;
-    p.n_items = (uint32_t)(chunks * p.tile_items);
+    int rc = ChunkSchedule(t, p.frame_begin, p.n_frames, p.tile_items, resident, p.cam.sqrt_spp);
+    if (rc != RT2_OK) return rc;
+    p.chunks = t->d_chunks;
+    p.n_chunks = t->n_chunks;
+    p.n_items = t->n_chunks * p.tile_items;
     p.batch_max = (uint32_t)t->batch_max;
     p.batch_div = (uint32_t)std::max<int64_t>(1, (resident / 64) * 2);  // half of the left work / waves
     int grid = (int)std::min<int64_t>(resident, (int64_t)p.n_items) / RenderBlockSize();
     grid = std::max(grid, 1);
     t->last_grid = grid;
-    t->last_chunk_frames = p.chunk_frames;
+    t->last_chunk_frames = t->first_chunk_frames;
     HIP_TRY(hipMemsetAsync(t->d_work, 0, sizeof(uint32_t), t->stream));
     hipEvent_t e0 = TakeEvent(t), e1 = TakeEvent(t);
     if (e0) HIP_TRY(hipEventRecord(e0, t->stream));

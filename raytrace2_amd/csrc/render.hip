@@ -5,16 +5,21 @@
 // PerlinNoiseGen.cpp:54-88), as one persistent gfx950 kernel.
 //
 // Execution model (MI355X):
-//  * one lane = one pixel for a whole launch; a lane renders that pixel's frames
-//    [frame_begin, frame_begin + n_frames) back to back and accumulates them in registers in
-//    frame order, so the float sum is the reference's `accumulation_data_[i] += c` sequence;
+//  * persistent lanes take work items = (pixel, chunk of consecutive frames of the launch); a lane
+//    renders its chunk's frames back to back and writes each frame's sample (float3) to the
+//    per-frame sample buffer; accumulate_kernel then adds a launch's samples to the accumulation in
+//    frame order, so the float sum is the reference's `accumulation_data_[i] += c` sequence
+//    (RayTracer.cpp:64) whatever the chunking;
 //  * one loop iteration = one bounce for every live lane; a lane whose path ends starts its next
 //    frame in the same iteration (path regeneration), so lanes never idle inside a wave until
-//    their pixel is done;
-//  * pixels are handed out in 8x8 tiles by a wave-aggregated atomic: __ballot of the lanes that
-//    need work, one atomicAdd per wave, a popcount prefix for each lane's slot;
-//  * the traversal stack lives in LDS (lane-major columns: a wave's push/pop is one
-//    conflict-free ds_write/ds_read); scenes up to kLdsSceneBytesMax are staged in LDS as well;
+//    their chunk is done;
+//  * items are numbered chunk-major over 8x8 pixel tiles and handed out by a wave-aggregated
+//    atomic: __ballot of the lanes that need work, one atomicAdd per wave batch (guided sizes), a
+//    popcount prefix for each lane's slot;
+//  * small scenes run a threaded (stackless) pre-order program walked in lockstep by the wave, so
+//    step kinds are wave-uniform and records come through scalar loads; larger ones use a stack
+//    traversal with the stack in LDS (lane-major columns: a wave's push/pop is one conflict-free
+//    ds_write/ds_read) and the scene, or the top of its BVH, staged in LDS beside it;
 //  * traversal carries only (t, primitive ref, transform ref) of the closest hit; the hit point,
 //    normal and material are computed once for the winning primitive (bit-identical to computing
 //    them at every candidate hit, as the reference does);
@@ -64,6 +69,9 @@ constexpr int kBlock = 256;
 #endif
 #ifndef RT2_EXP_STAMPS
 #define RT2_EXP_STAMPS 0  // diagnostic build: per-section s_memtime sums into the stamp slots
+#endif
+#ifndef RT2_EXP_ENDTIME
+#define RT2_EXP_ENDTIME 0  // diagnostic build: per-wave start / first-idle / end times (s_memrealtime) into diag
 #endif
 #ifndef RT2_WIDE_PROGRAM
 #define RT2_WIDE_PROGRAM 1  // threaded program: 64-byte steps (entry + first 48 record bytes, one load)
@@ -138,6 +146,8 @@ __device__ __forceinline__ f3 recip3(f3 d) {
   return mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
 }
 __device__ __forceinline__ f3 xyz(float4 v) { return mk(v.x, v.y, v.z); }
+// floor(n / d) for n < 2^31 by the host's multiplier (rt2_layout.h Magic): v_mad_u64_u32 + shift
+__device__ __forceinline__ uint32_t udiv(uint32_t n, Magic d) { return (uint32_t)(((uint64_t)n * d.m) >> d.s); }
 __device__ __forceinline__ uint32_t bits(float f) { return __float_as_uint(f); }
 // glm scalar max/min
 __device__ __forceinline__ float gmax(float x, float y) { return (x < y) ? y : x; }
@@ -1272,10 +1282,8 @@ __device__ __forceinline__ uint32_t local_index(const RenderParams& P, uint32_t 
   const uint32_t x = xy & 0xFFFFu, y = xy >> 16;
   uint32_t r = y;
   if (P.world > 1) {
-    uint32_t bh = (uint32_t)P.band_h, bw = bh * (uint32_t)P.world;
-    asm volatile("" : "+s"(bh), "+s"(bw));  // per-call reciprocals (see camera_ray)
-    const uint32_t q = y / bw;
-    r = q * bh + (y - (y / bh) * bh);
+    const uint32_t bh = (uint32_t)P.band_h;
+    r = udiv(y, P.div_band_w) * bh + (y - udiv(y, P.div_band_h) * bh);
   }
   return r * (uint32_t)P.width + x;
 }
@@ -1311,7 +1319,6 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
   const int lane = (int)__lane_id();
   const float4* M = reinterpret_cast<const float4*>(P.materials);
   const f3 bg = mk(P.background[0], P.background[1], P.background[2]);
-  const int frame_end = P.frame_begin + P.n_frames;
   bool need = true;   // lane wants a work item
   bool idle = false;  // no work left for this lane: it stays in the loop, masked, until the wave ends,
                       // so the loop head is a convergence point and wave totals stay in SGPRs
@@ -1332,6 +1339,10 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
   const uint32_t max_depth = (uint32_t)P.max_depth;  // <= 0xFFFF (rt2_tracer_set_max_depth)
   Counters cnt = {};
   bool overflow = false;
+#if RT2_EXP_ENDTIME
+  const unsigned long long et_start = __builtin_amdgcn_s_memrealtime();
+  unsigned long long et_idle = 0;  // first loop head at which a lane of this wave found no work
+#endif
 
 #if RT2_EXP_STAMPS
   unsigned long long st_fetch = 0, st_trace = 0, st_shade = 0, st_finish = 0, st_t;
@@ -1380,26 +1391,28 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
         if (item >= P.n_items) {
           idle = true;  // no work left for this lane
         } else {
-          const uint32_t chunk = item / P.tile_items;  // chunk-major: every tile's chunk 0 first
+          const uint32_t chunk = udiv(item, P.div_tile_items);  // chunk-major: every tile's chunk 0 first
           const uint32_t titem = item - chunk * P.tile_items;
-          uint32_t tile = titem >> 6, within = titem & 63u;
-          int x = (int)((tile % (uint32_t)P.tiles_x) * 8u + (within & 7u));
-          int r = (int)((tile / (uint32_t)P.tiles_x) * 8u + (within >> 3));
-          int f = P.frame_begin + (int)chunk * P.chunk_frames;
-          const int fstop = min(f + P.chunk_frames, frame_end);  // chunk_frames <= 0x10000
-          if (x < P.width && r < P.local_rows && f < fstop) {  // else: partial edge tile, or no frames
-            int y = ((r / P.band_h) * P.world + P.rank) * P.band_h + (r % P.band_h);
-            path.xy = (uint32_t)x | ((uint32_t)y << 16);
+          const uint32_t tile = titem >> 6, within = titem & 63u;
+          const uint32_t trow = udiv(tile, P.div_tiles_x);
+          const int x = (int)((tile - trow * (uint32_t)P.tiles_x) * 8u + (within & 7u));
+          const int r = (int)(trow * 8u + (within >> 3));
+          // the chunk's first frame and its stratum (RayTracer.cpp:59-60, from the host's table),
+          // and the next chunk's first frame (<= first + 0x10000)
+          const uint32_t* ce = P.chunks + 2u * chunk;
+          const int f = (int)ce[0];
+          const int fstop = (int)ce[2];
+          if (x < P.width && r < P.local_rows) {  // else: a lane of a partial edge tile
+            uint32_t y = (uint32_t)r;
+            if (P.world > 1) {  // local row -> global row of the interleaved band partition
+              const uint32_t b = udiv((uint32_t)r, P.div_band_h);
+              y = (b * (uint32_t)P.world + (uint32_t)P.rank) * (uint32_t)P.band_h + ((uint32_t)r - b * (uint32_t)P.band_h);
+            }
+            path.xy = (uint32_t)x | (y << 16);
             item_rays = 0;
             need = false;
             path.start((uint32_t)f);
-            {  // stratum (RayTracer.cpp:59-60): s_i = f % sq, s_j = (f / sq) % sq; then advanced per frame
-              // (divisor opaque here: a reciprocal hoisted out of the render loop would hold a VGPR)
-              uint32_t sq = (uint32_t)P.cam.sqrt_spp;
-              asm volatile("" : "+s"(sq));
-              const uint32_t fq = (uint32_t)f / sq;
-              path.sij = ((uint32_t)f - fq * sq) | ((fq % sq) << 16);
-            }
+            path.sij = ce[1];  // then advanced per frame below
             camera_ray<F>(P, path, ro, rd, rtime);
             thr = mk(1, 1, 1);
             dl = max_depth | ((uint32_t)(fstop - f - 1) << 16);
@@ -1407,6 +1420,9 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
         }
       }
     }
+#if RT2_EXP_ENDTIME
+    if (et_idle == 0ull && __ballot(idle) != 0ull) et_idle = __builtin_amdgcn_s_memrealtime();
+#endif
     if (__ballot(!idle) == 0ull) break;  // the wave is done (uniform exit)
     rays += (unsigned long long)__popcll(__ballot(!need && (dl & 0xFFFFu) != 0u));  // RayColor casts below
     if (need) continue;
@@ -1576,6 +1592,20 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
   if (overflow) atomicAdd(P.stats + StatsCounters::kCount, 1ull);  // overflow flag slot
 #if RT2_EXP_WAVESTEPS
   for (int k = 0; k < 8; k++) atomicAdd(P.stats + StatsCounters::kDiag + k, (unsigned long long)cnt.wd[k]);
+#endif
+#if RT2_EXP_ENDTIME
+  if (lane == 0) {  // minima as maxima of complements (the slots start at 0); 100 MHz ticks
+    const unsigned long long et_end = __builtin_amdgcn_s_memrealtime();
+    unsigned long long* d = P.stats + StatsCounters::kDiag;
+    atomicMax(d + 0, ~et_start);
+    atomicMax(d + 1, et_start);
+    atomicMax(d + 2, ~et_idle);
+    atomicMax(d + 3, et_end);
+    atomicAdd(d + 4, et_end - et_idle);
+    atomicAdd(d + 5, et_end - et_start);
+    atomicAdd(d + 6, 1ull);
+    atomicMax(d + 7, et_idle);
+  }
 #endif
 }
 

@@ -148,6 +148,13 @@ struct StatsCounters {  // u64 slots written by the kernel
 };
 constexpr int kStatsSlots = StatsCounters::kSlots;
 
+// floor(n / d) = (n * m) >> s for every 0 <= n < 2^31 (Granlund-Montgomery: m = ceil(2^(31+l) / d),
+// s = 31 + l, 2^(l-1) < d <= 2^l, so m < 2^32): one 32x32->64 multiply and a shift instead of a
+// division by a run-time divisor. Built by the host (MakeMagic, capi.cpp).
+struct Magic {
+  uint32_t m, s;
+};
+
 struct RenderParams {
   const void* nodes;      // float4[]
   const void* materials;  // float4[]
@@ -166,7 +173,14 @@ struct RenderParams {
   uint32_t batch_max;      // most work items a wave reserves at once
   uint32_t batch_div;      // a wave reserves (items left) / batch_div, at least what it needs
   int frame_begin, n_frames, max_depth;
-  int chunk_frames;        // frames per work item; chunk c = [frame_begin + c*chunk_frames, ...)
+  // Frame chunks of the launch, (first frame, stratum s_i | s_j << 16 of that frame) per chunk
+  // (RayTracer.cpp:59-60) and a sentinel (frame_begin + n_frames, 0): chunk c is the frames
+  // [chunks[2c], chunks[2c + 2]). Work item = one pixel x one chunk; chunks shrink toward the end
+  // of the launch so the last items are short (capi.cpp, ChunkSchedule).
+  const uint32_t* chunks;
+  uint32_t n_chunks;
+  Magic div_tile_items, div_tiles_x;  // item -> (chunk, tile), tile -> tile row
+  Magic div_band_h, div_band_w;       // band_h and band_h * world (row-band partition)
   uint32_t seed_lo, seed_hi;
   float* samples;          // float3 per (launch frame, local pixel): [n_frames][local pixels][3]
   uint32_t local_pixels;   // width * local_rows
