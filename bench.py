@@ -69,7 +69,7 @@ def parse():
     ap.add_argument("--spp", type=int, default=1000)
     ap.add_argument("--max-depth", type=int, default=50)
     ap.add_argument("--seed", type=int, default=0x5EED2024)
-    ap.add_argument("--band-h", type=int, default=16)
+    ap.add_argument("--band-h", type=int, default=2, help="row-band height of the multi-GPU partition")
     ap.add_argument("--launch-frames", type=int, default=0, help="frames per kernel launch (0 = all)")
     ap.add_argument("--work-split", type=int, default=-1,
                     help="work items (pixel x frame chunk) per resident lane (-1: library default, 0: no split)")

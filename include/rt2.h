@@ -8,8 +8,9 @@
  * status and never throws; rt2_last_error() has the message (thread-local).
  *
  * Pixel layout: row-major, row 0 = bottom image row (RayTracer.cpp:97-102). With a row-band
- * partition (rt2_tracer_set_partition) a tracer owns the "local rows" y with
- * (y / band_h) % world == rank, stored compactly in increasing y.
+ * partition (rt2_tracer_set_partition) a tracer owns the "local rows" y whose band b = y / band_h
+ * has (b % world + b / world) % world == rank (one band per period of `world` bands, the phase
+ * rotating by one each period), stored compactly in increasing y.
  */
 #ifndef RT2_H_
 #define RT2_H_
@@ -164,7 +165,7 @@ RT2_API int rt2_tracer_get_camera(const rt2_tracer* tr, rt2_camera_desc* out);
  * one exchange is an RCCL gather (ncclGather over xGMI) of every GPU's band stack to the root GPU,
  * where a kernel de-interleaves it into the full image. The result is bit-identical to one GPU.
  *
- * (1) One process driving n GPUs: rt2_tracer_create_multi (devices NULL = 0..n-1; band_h 0 = 16),
+ * (1) One process driving n GPUs: rt2_tracer_create_multi (devices NULL = 0..n-1; band_h 0 = 2),
  *     one RCCL communicator per device (ncclCommInitAll). Every rt2_tracer_* function works on it as
  *     on a one-GPU tracer; readbacks (accumulation, non_converted_pixels, pixels, pixels_async,
  *     ray_counts, copy_accum_device) return the FULL image (local_rows = height), gathering first.

@@ -161,7 +161,7 @@ inline void WriteImage(const std::vector<vec3>& pixels, int width, int height, c
 }  // namespace util
 
 // cpu::RayTracer (RayTracer.hpp:15-42) on MI355X GPUs: one GPU (`device`; n_gpus 0), or `n_gpus`
-// GPUs starting at `device` with an RCCL gather of their row bands (band_h 0 = 16 rows; n_gpus 1
+// GPUs starting at `device` with an RCCL gather of their row bands (band_h 0 = 2 rows; n_gpus 1
 // is the same path with a communicator of size 1).
 class RayTracer {
  public:

@@ -140,7 +140,8 @@ class OracleScene:
                rank=0, world=1, accum=None, ray_counts=None, threads=0, forward=False):
         """Frames [frame_begin, frame_begin+frames) of RayTracer::Update (RayTracer.cpp:55-70)."""
         seed = self.seed if seed is None else seed
-        rows = [y for y in range(h) if (y // (band_h or h)) % world == rank]
+        bh = band_h or h
+        rows = [y for y in range(h) if ((y // bh) % world + (y // bh) // world) % world == rank]
         if accum is None:
             accum = np.zeros((len(rows), w, 3), np.float32)
         if ray_counts is None:

@@ -1497,8 +1497,8 @@ void oracle_transform(const float* in, float* model, float* inv) {
 
 // Render frames [frame_begin, frame_begin + n_frames) of the scene at W x H (OnResize dims) with
 // the camera's samples_per_pixel = spp (sets the stratification), accumulating into `accum`
-// (float3 per pixel, rank-local compact rows: row r of this rank is global row
-// y = ((r / band_h) * world + rank) * band_h + r % band_h). ray_counts (nullable) += rays/pixel.
+// (float3 per pixel, rank-local compact rows: the rows y whose band b = y / band_h has
+// (b % world + b / world) % world == rank, in increasing y). ray_counts (nullable) += rays/pixel.
 // forward != 0 selects RayColorForward (GPU product order).
 int oracle_render(void* sp, int W, int H, int spp, int max_depth, uint64_t seed, int frame_begin, int n_frames,
                   int band_h, int rank, int world, float* accum, uint32_t* ray_counts, int threads, int forward,
@@ -1515,7 +1515,7 @@ int oracle_render(void* sp, int W, int H, int spp, int max_depth, uint64_t seed,
   // rank-local rows
   std::vector<int> rows;
   for (int y = 0; y < H; y++)
-    if ((y / band_h) % world == rank) rows.push_back(y);
+    if ((y / band_h % world + y / band_h / world) % world == rank) rows.push_back(y);  // BandRank
   if (threads <= 0) threads = (int)std::max(1u, std::thread::hardware_concurrency());
   std::atomic<size_t> next{0};
   std::vector<Counters> cnts((size_t)threads);

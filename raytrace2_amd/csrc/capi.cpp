@@ -124,6 +124,13 @@ struct rt2_tracer {
 
 namespace {
 
+// Row-band height of the multi-GPU partitions (band_h 0). Measured, 8-way split emulated rank by rank
+// on one MI355X (job rate = all ranks' rays / the slowest rank's time), band heights 8 / 4 / 2 / 1:
+// Cornell 190 / 193 / 197 / 198 k Mray/s, book 1 55.9 / 57.5 / 54.9 / 54.6 k, Cornell volume
+// 119.6 / - / 121.5 / 122.4 k, book 2 9.89 / - / 10.15 / 9.81 k. Narrow bands balance the ranks
+// (image cost varies smoothly with the row); 2 rows (32x2 work tiles) is within 1-5 % of the best.
+constexpr int kDefaultBandH = 2;
+
 thread_local std::string g_err;
 
 int Fail(int code, const std::string& m) {
@@ -148,7 +155,7 @@ int HipFail(hipError_t e, const char* what) {
 int LocalRows(int h, int band_h, int rank, int world) {
   int n = 0;
   for (int y = 0; y < h; y++)
-    if ((y / band_h) % world == rank) n++;
+    if (BandRank(y / band_h, world) == rank) n++;
   return n;
 }
 
@@ -818,12 +825,17 @@ int LaunchFrames(rt2_tracer* t, int n_frames) {
   p.band_h = t->band_h > 0 ? t->band_h : t->height;
   p.rank = t->rank;
   p.world = t->world;
-  p.tiles_x = (t->width + 7) / 8;
-  p.tile_items = (uint32_t)p.tiles_x * (uint32_t)((t->local_rows + 7) / 8) * 64u;
+  // work tiles of 64 pixels: 8x8, or as tall as a row band narrower than 8 rows (16x4, 32x2, 64x1)
+  // so that a wave's pixels stay in one band (neighbouring pixels, coherent primary rays)
+  const int tile_rows = t->world > 1 && p.band_h < 8 ? (p.band_h >= 4 ? 4 : p.band_h >= 2 ? 2 : 1) : 8;
+  p.tile_shift = tile_rows == 8 ? 3u : tile_rows == 4 ? 4u : tile_rows == 2 ? 5u : 6u;
+  p.tiles_x = (t->width + (1 << p.tile_shift) - 1) >> p.tile_shift;
+  p.tile_items = (uint32_t)p.tiles_x * (uint32_t)((t->local_rows + tile_rows - 1) / tile_rows) * 64u;
   p.div_tile_items = MakeMagic(p.tile_items);
   p.div_tiles_x = MakeMagic((uint32_t)p.tiles_x);
   p.div_band_h = MakeMagic((uint32_t)p.band_h);
   p.div_band_w = MakeMagic((uint32_t)p.band_h * (uint32_t)p.world);
+  p.div_world = MakeMagic((uint32_t)p.world);
   p.local_pixels = (uint32_t)t->width * (uint32_t)t->local_rows;
   p.max_depth = t->max_depth;
   p.seed_lo = (uint32_t)t->seed;
@@ -1240,7 +1252,9 @@ int rt2_tracer_ray_counts(rt2_tracer* t, uint32_t* out) {
       if (rc != RT2_OK) return rc;
       const int bh = BandH(p);
       for (int r = 0; r < p->local_rows; r++) {
-        const int y = ((r / bh) * p->world + p->rank) * bh + r % bh;
+        const int period = r / bh;  // the rank's band of this period (rt2_layout.h BandRank)
+        const int phase = ((p->rank - period) % p->world + p->world) % p->world;
+        const int y = (period * p->world + phase) * bh + r % bh;
         memcpy(out + (size_t)y * p->width, part.data() + (size_t)r * p->width, (size_t)p->width * sizeof(uint32_t));
       }
     }
@@ -1329,7 +1343,7 @@ int rt2_tracer_create_multi(const rt2_scene* s, int n, const int* devices, int b
     return Fail(RT2_ERR_INVALID, "rt2_tracer_create_multi: devices must be distinct (or all one GPU, for tests)");
   auto m = std::make_unique<rt2_tracer>();
   m->loopback = n > 1 && all_same;
-  const int bh = band_h > 0 ? band_h : 16;
+  const int bh = band_h > 0 ? band_h : kDefaultBandH;
   auto cleanup = [&](int rc) {
     for (rt2_tracer* p : m->parts) rt2_tracer_destroy(p);
     m->parts.clear();
@@ -1369,7 +1383,7 @@ int rt2_tracer_join(rt2_tracer* t, const uint8_t* unique_id, int world, int rank
   if (!t || !unique_id) return Fail(RT2_ERR_INVALID, "rt2_tracer_join: null argument");
   if (IsMulti(t)) return Fail(RT2_ERR_INVALID, "rt2_tracer_join: a multi-GPU tracer has its own communicators");
   if (t->comm) return Fail(RT2_ERR_INVALID, "rt2_tracer_join: already joined");
-  int rc = rt2_tracer_set_partition(t, band_h > 0 ? band_h : 16, rank, world);
+  int rc = rt2_tracer_set_partition(t, band_h > 0 ? band_h : kDefaultBandH, rank, world);
   if (rc != RT2_OK) return rc;
   ncclUniqueId id;
   memcpy(&id, unique_id, sizeof(id));

@@ -1,6 +1,6 @@
 // gather.hip — root side of the multi-GPU image gather.
 //
-// Every GPU renders the interleaved row bands of its rank (band b -> rank b % world) into a compact
+// Every GPU renders the interleaved row bands of its rank (rt2_layout.h BandRank) into a compact
 // band stack; the stacks, padded to the same height, arrive on the root one after another
 // ([world][max_rows][W] float3, by ncclGather or device-local copies). This kernel writes them
 // back to image order and derives Pixels() = ToColor(clamp(accum / frame_idx, 0, 1))
@@ -26,8 +26,9 @@ __global__ __launch_bounds__(256) void deinterleave_kernel(const float* __restri
   if (i >= npix) return;
   const uint32_t y = i / width, x = i - y * width;
   const uint32_t band = y / band_h;
-  const uint32_t rank = band % world;
-  const uint32_t row = (band / world) * band_h + (y - band * band_h);  // rank-local row
+  const uint32_t period = band / world;
+  const uint32_t rank = (band - period * world + period) % world;  // rt2_layout.h BandRank
+  const uint32_t row = period * band_h + (y - band * band_h);       // rank-local row
   const float* s = stacks + 3ull * (((unsigned long long)rank * max_rows + row) * width + x);
   const float a0 = s[0], a1 = s[1], a2 = s[2];
   image[3ull * i] = a0;

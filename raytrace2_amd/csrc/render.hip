@@ -1276,8 +1276,9 @@ __device__ __forceinline__ void camera_ray(const RenderParams& P, Path& g, f3& o
   d = normalize(pc - c);
 }
 
-// Local (row-band) pixel index of global pixel xy: global row y belongs to band y / band_h, owned by
-// rank (y / band_h) % world and stored as local row (y / (band_h * world)) * band_h + y % band_h.
+// Local (row-band) pixel index of global pixel xy: global row y lies in band y / band_h of period
+// y / (band_h * world) and is stored as local row (y / (band_h * world)) * band_h + y % band_h
+// (rt2_layout.h BandRank).
 __device__ __forceinline__ uint32_t local_index(const RenderParams& P, uint32_t xy) {
   const uint32_t x = xy & 0xFFFFu, y = xy >> 16;
   uint32_t r = y;
@@ -1395,8 +1396,10 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
           const uint32_t titem = item - chunk * P.tile_items;
           const uint32_t tile = titem >> 6, within = titem & 63u;
           const uint32_t trow = udiv(tile, P.div_tiles_x);
-          const int x = (int)((tile - trow * (uint32_t)P.tiles_x) * 8u + (within & 7u));
-          const int r = (int)(trow * 8u + (within >> 3));
+          // tiles of (64 >> tile_shift) local rows x (1 << tile_shift) pixels
+          const uint32_t tw = 1u << P.tile_shift;
+          const int x = (int)((tile - trow * (uint32_t)P.tiles_x) * tw + (within & (tw - 1u)));
+          const int r = (int)(trow * (64u >> P.tile_shift) + (within >> P.tile_shift));
           // the chunk's first frame and its stratum (RayTracer.cpp:59-60, from the host's table),
           // and the next chunk's first frame (<= first + 0x10000)
           const uint32_t* ce = P.chunks + 2u * chunk;
@@ -1404,9 +1407,11 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
           const int fstop = (int)ce[2];
           if (x < P.width && r < P.local_rows) {  // else: a lane of a partial edge tile
             uint32_t y = (uint32_t)r;
-            if (P.world > 1) {  // local row -> global row of the interleaved band partition
-              const uint32_t b = udiv((uint32_t)r, P.div_band_h);
-              y = (b * (uint32_t)P.world + (uint32_t)P.rank) * (uint32_t)P.band_h + ((uint32_t)r - b * (uint32_t)P.band_h);
+            if (P.world > 1) {  // local row -> global row (rt2_layout.h BandRank)
+              const uint32_t per = udiv((uint32_t)r, P.div_band_h);  // the rank's band in period `per`
+              const uint32_t pm = per - udiv(per, P.div_world) * (uint32_t)P.world;
+              const uint32_t phase = (uint32_t)P.rank >= pm ? (uint32_t)P.rank - pm : (uint32_t)P.rank + (uint32_t)P.world - pm;
+              y = (per * (uint32_t)P.world + phase) * (uint32_t)P.band_h + ((uint32_t)r - per * (uint32_t)P.band_h);
             }
             path.xy = (uint32_t)x | (y << 16);
             item_rays = 0;

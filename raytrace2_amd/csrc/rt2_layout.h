@@ -33,6 +33,13 @@ inline constexpr bool is_acc_bvh(uint32_t kind) { return kind - kAccBvh < 3u; }
 constexpr int kListAccelMin = 32;  // leaf-only sphere lists at least this long get a tree
 
 constexpr uint32_t kRefNone = 0xFFFFFFFFu;
+
+// Row-band partition of the image over `world` GPUs: rows in bands of band_h; band b lies in
+// period p = b / world at phase q = b % world and belongs to rank (q + p) % world. Every rank owns
+// one band per period (interleaving spreads costly image regions), and the phase a rank takes
+// rotates from period to period, so no rank is tied to one phase of a periodic cost pattern. A rank
+// stores its rows compactly in increasing y: local row l = p * band_h + (y % band_h).
+inline constexpr int BandRank(int band, int world) { return (band % world + band / world) % world; }
 constexpr uint32_t kOffsetMask = 0x0FFFFFFFu;
 inline constexpr uint32_t make_ref(uint32_t kind, uint32_t off) { return (kind << 28) | off; }
 
@@ -167,8 +174,9 @@ struct RenderParams {
   int width, height;       // global image
   int local_rows;          // rows owned by this rank
   int band_h, rank, world; // interleaved row bands: global band b -> rank b % world
-  int tiles_x;             // ceil(width / 8)
-  uint32_t tile_items;     // tiles_x * ceil(local_rows / 8) * 64: lanes of one frame chunk
+  uint32_t tile_shift;     // work tiles of 64 pixels: (1 << tile_shift) wide x (64 >> tile_shift) local rows
+  int tiles_x;             // ceil(width / tile width)
+  uint32_t tile_items;     // tiles_x * ceil(local_rows / tile rows) * 64: lanes of one frame chunk
   uint32_t n_items;        // tile_items * chunks (work item = one pixel x one chunk of frames)
   uint32_t batch_max;      // most work items a wave reserves at once
   uint32_t batch_div;      // a wave reserves (items left) / batch_div, at least what it needs
@@ -180,7 +188,7 @@ struct RenderParams {
   const uint32_t* chunks;
   uint32_t n_chunks;
   Magic div_tile_items, div_tiles_x;  // item -> (chunk, tile), tile -> tile row
-  Magic div_band_h, div_band_w;       // band_h and band_h * world (row-band partition)
+  Magic div_band_h, div_band_w, div_world;  // band_h, band_h * world, world (row-band partition)
   uint32_t seed_lo, seed_hi;
   float* samples;          // float3 per (launch frame, local pixel): [n_frames][local pixels][3]
   uint32_t local_pixels;   // width * local_rows

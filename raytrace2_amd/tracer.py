@@ -166,10 +166,16 @@ class SceneLoader:
             return None
 
 
+def band_rank(band: int, world: int) -> int:
+    """Rank owning row band `band` (rt2_layout.h BandRank): period p = band // world, phase
+    q = band % world, rank (q + p) % world — one band per period per rank, phases rotating."""
+    return (band % world + band // world) % world
+
+
 def local_rows(height: int, band_h: int, rank: int, world: int) -> List[int]:
-    """Global rows owned by `rank` under the interleaved row-band partition (band b -> b % world)."""
+    """Global rows owned by `rank` under the interleaved row-band partition, in increasing y."""
     bh = band_h if band_h > 0 else height
-    return [y for y in range(height) if (y // bh) % world == rank]
+    return [y for y in range(height) if band_rank(y // bh, world) == rank]
 
 
 def assemble_bands(parts: Sequence[np.ndarray], height: int, band_h: int) -> np.ndarray:
@@ -303,7 +309,7 @@ class RayTracer:
     def n_gpus(self) -> int:
         return int(check(lib.rt2_tracer_n_gpus(self._h)))
 
-    def join(self, unique_id: bytes, world: int, rank: int, band_h: int = 16) -> None:
+    def join(self, unique_id: bytes, world: int, rank: int, band_h: int = 0) -> None:
         """rt2_tracer_join: partition (band_h, rank, world) + this rank of an RCCL communicator."""
         buf = (ctypes.c_uint8 * UNIQUE_ID_BYTES).from_buffer_copy(unique_id[:UNIQUE_ID_BYTES])
         check(lib.rt2_tracer_join(self._h, buf, int(world), int(rank), int(band_h)))

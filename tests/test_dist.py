@@ -53,3 +53,18 @@ def test_gloo_band_gather_equals_single_render(tmp_path, world):
     from oracle.oracle import OracleScene
     full, _, _ = OracleScene(scene_path("cornell_box_original")).render(W, H, SPP, FRAMES, forward=True)
     assert np.array_equal(img.view(np.uint32), full.view(np.uint32))
+
+
+@pytest.mark.parametrize("h,band_h,world", [(45, 8, 3), (1024, 16, 8), (800, 16, 8), (1024, 8, 8), (10, 8, 4), (7, 1, 7)])
+def test_band_partition_covers_every_row_once(h, band_h, world):
+    """rt2_layout.h BandRank: the ranks' rows are disjoint, cover the image, and every rank owns one
+    band of each full period, its phase rotating by one per period."""
+    from raytrace2_amd.tracer import band_rank, local_rows
+    parts = [local_rows(h, band_h, r, world) for r in range(world)]
+    assert sorted(y for p in parts for y in p) == list(range(h))
+    assert max(map(len, parts)) - min(map(len, parts)) <= band_h
+    bands = -(-h // band_h)
+    for p in range(bands // world):
+        owners = [band_rank(p * world + q, world) for q in range(world)]
+        assert sorted(owners) == list(range(world))
+        assert owners[0] == p % world

@@ -80,6 +80,12 @@ def test_c5_book2_full_width_band():
     _check("book2_final_scene_10000_samples", 800, 800, 10000, 24, band_h=8, rank=50, world=100)
 
 
+@pytest.mark.parametrize("band_h", [1, 2, 4])
+def test_c2_narrow_bands(band_h):
+    """Row bands narrower than a work tile (tiles of 64x1, 32x2, 16x4 pixels): rank 5 of 8."""
+    _check("cornell_box_original", 1024, 1024, 1000, 40, band_h=band_h, rank=5, world=8)
+
+
 def test_c2_headline_last_frames_full_width():
     """The headline's wrap region on a wider band: frames 950..999 continued from the GPU."""
     _check_continuation("cornell_box_original", 1024, 1024, 1000, 950, 1000, band_h=64, rank=7, world=16)

@@ -72,7 +72,7 @@ def test_one_gpu_through_rccl_is_bit_identical():
     assert _same(ncp, acc / np.float32(frames))
 
 
-@pytest.mark.parametrize("n,band_h", [(2, 8), (3, 8), (8, 4), (8, 16)])
+@pytest.mark.parametrize("n,band_h", [(2, 8), (3, 8), (8, 4), (8, 16), (4, 1), (5, 2), (3, 5)])
 def test_partitions_on_one_gpu_reassemble(n, band_h):
     """n row-band partitions (uneven: 45 rows) gathered and de-interleaved equal one render."""
     w, h, spp, frames = 50, 45, 16, 5
