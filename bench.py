@@ -203,7 +203,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     share = os.environ.get("RT2_BENCH_SHARE_GPU") == "1"  # rehearsal: every rank on GPU 0, gather via gloo
-    if world > 1:
+    # RT2_BENCH_RANKS=1: the one-process-per-GPU path even at WORLD_SIZE 1 (join + gather, comm of size 1)
+    if world > 1 or os.environ.get("RT2_BENCH_RANKS") == "1":
         mode = "ranks"
         if a.gpus not in (1, world):
             raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}")
