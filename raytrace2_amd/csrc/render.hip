@@ -200,28 +200,35 @@ struct Nodes {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
+// (offsets are wave-uniform by construction; readfirstlane keeps them in SGPRs even where the
+// compiler could not prove it, and costs nothing where it could)
 __device__ __forceinline__ uint32_t sld1(const void* base, uint32_t off) {
+  off = __builtin_amdgcn_readfirstlane(off);
   uint32_t v;
   asm("s_load_dword %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(base), "s"(off));
   return v;
 }
 __device__ __forceinline__ u32x4 sld4(const void* base, uint32_t off) {
+  off = __builtin_amdgcn_readfirstlane(off);
   u32x4 v;
   asm("s_load_dwordx4 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(base), "s"(off));
   return v;
 }
 __device__ __forceinline__ u32x8 sld8(const void* base, uint32_t off) {
+  off = __builtin_amdgcn_readfirstlane(off);
   u32x8 v;
   asm("s_load_dwordx8 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(base), "s"(off));
   return v;
 }
 __device__ __forceinline__ u32x16 sld16(const void* base, uint32_t off) {
+  off = __builtin_amdgcn_readfirstlane(off);
   u32x16 v;
   asm("s_load_dwordx16 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(base), "s"(off));
   return v;
 }
 // 20 dwords (one quad record) at off
 __device__ __forceinline__ void sld20(const void* base, uint32_t off, u32x16& a, u32x4& b) {
+  off = __builtin_amdgcn_readfirstlane(off);
   asm("s_load_dwordx16 %0, %2, %3\n\ts_load_dwordx4 %1, %2, %4\n\ts_waitcnt lgkmcnt(0)"
       : "=&s"(a), "=&s"(b)
       : "s"(base), "s"(off), "s"(off + 64u));
@@ -350,8 +357,9 @@ __device__ __forceinline__ f3 refract(f3 uv, f3 n, float etai_over_etat) {
 struct Counters {
   uint32_t bvh, quad, sphere, xform, medium, list;
 #if RT2_EXP_WAVESTEPS
-  // wave-level (counted by the first active lane): trace calls, steps, bvh, quad pairs, single
-  // quads, xform, xform exits, active lanes at trace (summed by every lane)
+  // wave-level (counted by the first active lane): trace calls, steps, bvh + acc-bvh steps, quad
+  // runs, sphere + acc-sphere steps, media, extra trips of the min-index search, active lanes at
+  // trace (summed by every lane)
   uint32_t wd[8];
 #endif
 };
@@ -912,8 +920,16 @@ __device__ __forceinline__ bool trace_stack(const RenderParams& P, const Nodes<k
 #if RT2_WIDE_PROGRAM
 #define RT2_STEP_WORDS(w) const u32x16& w = sw
 #else
-#define RT2_STEP_WORDS(w) const u32x16 w = sld16(P.lin_wide, i * 64u)
+#define RT2_STEP_WORDS(w) const u32x16 w = sld16(P.lin_wide, at * 64u)
 #endif
+// Smallest `next` over the wave's active lanes (one ballot per distinct smaller value).
+__device__ __forceinline__ uint32_t wave_min_next(uint32_t next) {
+  uint32_t i = __builtin_amdgcn_readfirstlane(next);
+  unsigned long long lower;
+  while ((lower = __ballot(next < i)) != 0ull) i = __builtin_amdgcn_readlane(next, __ffsll((long long)lower) - 1);
+  return i;
+}
+
 template <uint32_t F, bool kStats>
 __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd, float time, Path& path, HitRef& h,
                                              Counters& cnt) {
@@ -939,48 +955,63 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
 #if RT2_EXP_WAVESTEPS
   cnt.wd[7]++;
 #endif
-  while (true) {
-    // wave-uniform step = min over live lanes of `next`
-    uint32_t i = __builtin_amdgcn_readfirstlane(next);
-    unsigned long long lower;
-    while ((lower = __ballot(next < i)) != 0ull) i = __builtin_amdgcn_readlane(next, __ffsll((long long)lower) - 1);
-    if (i >= len) break;
+  uint32_t i = wave_min_next(next);  // wave-uniform step = min over live lanes of `next`
+  while (i < len) {
 #if RT2_WIDE_PROGRAM
-    const u32x16 sw = sld16(P.lin_wide, i * 64u);  // entry + the first 48 bytes of its record
-    const u32x4 st = {sw[0], sw[1], sw[2], sw[3]};
+    u32x16 sw = sld16(P.lin_wide, i * 64u);  // entry + the first 48 bytes of its record
 #else
-    const u32x4 st = sld4(prog, i * 16u);
+    u32x16 sw;
+    {
+      const u32x4 e = sld4(prog, i * 16u);
+      sw[0] = e.x, sw[1] = e.y, sw[2] = e.z, sw[3] = e.w;
+      if (e.x == kBvh) {
+        const u32x8 b = sld8(recs, e.z * 16u);
+        for (int j = 0; j < 8; j++) sw[4 + j] = b[j];
+      }
+    }
 #endif
+    if (sw[0] == kBvh) {
+      // A run of BVH steps in a loop of its own: only `next` changes from step to step, so nothing
+      // else is carried (no register copies between kinds) and the step costs the slab test, the
+      // next-index update and the wave-minimum search.
+      const bool allfin = RT2_EXP_NO_FIN_AABB ? false : (bool)__all(fin);
+      do {
+        RT2_WAVE(1);
+        RT2_WAVE(2);
+        if (next == i) {
+          if (kStats) cnt.bvh++;
+          const float4 lo = make_float4(uf(sw[4]), uf(sw[5]), uf(sw[6]), 0.0f);
+          const float4 hi = make_float4(uf(sw[8]), uf(sw[9]), uf(sw[10]), 0.0f);
+          const bool in = allfin ? aabb_hit_fin(lo, hi, o, inv, tmin, tmax) : aabb_hit(lo, hi, o, inv, tmin, tmax);
+          next = in ? i + 1u : sw[1];
+        }
+        i = wave_min_next(next);
+        if (i >= len) break;
+#if RT2_WIDE_PROGRAM
+        sw = sld16(P.lin_wide, i * 64u);
+#else
+        const u32x4 e = sld4(prog, i * 16u);
+        sw[0] = e.x, sw[1] = e.y, sw[2] = e.z, sw[3] = e.w;
+        if (e.x == kBvh) {
+          const u32x8 b = sld8(recs, e.z * 16u);
+          for (int j = 0; j < 8; j++) sw[4 + j] = b[j];
+        }
+#endif
+      } while (sw[0] == kBvh);
+      if (i >= len) break;
+    }
+    const u32x4 st = {sw[0], sw[1], sw[2], sw[3]};
     const uint32_t kind = st.x, off = st.z;
     RT2_WAVE(1);
-    if (kind == kBvh) RT2_WAVE(2);
-    if (kind == kXform) RT2_WAVE(5);
-    if (kind == kXformExit) RT2_WAVE(6);
+    if (kind == kQuad) RT2_WAVE(3);
+    if (is_acc_bvh(kind)) RT2_WAVE(2);
+    if (kind == kSphere || kind == kAccSphere) RT2_WAVE(4);
+    if (kind == kMedium) RT2_WAVE(5);
+    const uint32_t at = i;
+    i = kRefNone;  // computed after the step
+    if (next == at) {
+    next = at + 1u;
     if (kind == kQuad) {
-#if RT2_EXP_WAVESTEPS
-      if ((int)__lane_id() == __builtin_amdgcn_readfirstlane((int)__lane_id())) {
-        cnt.wd[3] += st.w / 2u;
-        cnt.wd[4] += st.w & 1u;
-      }
-#endif
-    }
-    if (next != i) continue;
-    next = i + 1u;
-    if (kind == kBvh) {
-      if (kStats) cnt.bvh++;
-#if RT2_WIDE_PROGRAM
-      const u32x8 b = {sw[4], sw[5], sw[6], sw[7], sw[8], sw[9], sw[10], sw[11]};
-#else
-      const u32x8 b = sld8(recs, off * 16u);
-#endif
-      float4 lo = make_float4(uf(b[0]), uf(b[1]), uf(b[2]), 0.0f), hi = make_float4(uf(b[4]), uf(b[5]), uf(b[6]), 0.0f);
-#if RT2_EXP_NO_FIN_AABB
-      const bool in = aabb_hit(lo, hi, o, inv, tmin, tmax);
-#else
-      const bool in = __all(fin) ? aabb_hit_fin(lo, hi, o, inv, tmin, tmax) : aabb_hit(lo, hi, o, inv, tmin, tmax);
-#endif
-      if (!in) next = st.y;
-    } else if (kind == kQuad) {
       // a run of st.w quads with contiguous records, axis codes in st.y (3 bits each), tested in
       // order (issue-bound: one candidate at a time beats two interleaved, measured)
       const uint32_t run = st.w;
@@ -1021,7 +1052,7 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
           prim = make_ref(kind0, o0);
         }
       }
-      next = i + run;
+      next = at + run;
     } else if (Has<F, kFeatSphere>() && kind == kSphere) {
       float t;
       uint32_t ref = make_ref(kind, off);
@@ -1110,6 +1141,8 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
         h.xf = cur_xf;
       }
     }
+    }  // next == at
+    i = wave_min_next(next);
   }
   h.t = tmax;
   h.prim = prim;

@@ -10,7 +10,8 @@ sys.path.insert(0, ".")
 import raytrace2_amd as R  # noqa: E402
 
 scene = sys.argv[1] if len(sys.argv) > 1 else "scenes/cornell_box_original.json"
-w, h, spp, frames = 1024, 1024, 1000, int(sys.argv[2]) if len(sys.argv) > 2 else 16
+w, h = (int(v) for v in (sys.argv[3] if len(sys.argv) > 3 else "1024x1024").split("x"))
+spp, frames = (int(sys.argv[4]) if len(sys.argv) > 4 else 1000), int(sys.argv[2]) if len(sys.argv) > 2 else 16
 sc = R.Scene(scene)
 tr = R.RayTracer(sc, 0)
 tr.SetSamplesPerPixel(spp)
@@ -22,9 +23,11 @@ d = st["diag"]
 rays = st["rays"]
 wtrace = max(d[0], 1)
 out = {
-    "rays": rays, "lane_per_ray": {k: st[k] / rays for k in ("bvh_tests", "quad_tests", "xform_visits")},
+    "scene": scene, "rays": rays,
+    "lane_per_ray": {k: st[k] / rays for k in ("bvh_tests", "quad_tests", "sphere_tests", "xform_visits",
+                                                "medium_tests", "list_visits")},
     "wave_trace_calls": d[0], "active_lanes_per_trace": d[7] / wtrace,
-    "wave_per_trace": {"steps": d[1] / wtrace, "bvh": d[2] / wtrace, "quad_pairs": d[3] / wtrace,
-                       "quad_single": d[4] / wtrace, "xform": d[5] / wtrace, "xform_exit": d[6] / wtrace},
+    "wave_per_trace": {"steps": d[1] / wtrace, "bvh": d[2] / wtrace, "quad_runs": d[3] / wtrace,
+                       "spheres": d[4] / wtrace, "media": d[5] / wtrace, "min_search_extra_trips": d[6] / wtrace},
 }
 print(json.dumps(out, indent=1))
