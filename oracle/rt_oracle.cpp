@@ -1162,12 +1162,24 @@ Scene* LoadScene(const std::string& path, uint64_t seed, std::string& err) {
   bool legacy = prims && prims->t == J::Obj;
   std::vector<HPtr> top;
   if (legacy) {
-    // Legacy schema ({"spheres":[{center,radius,material_id,displacement?}]}): one scene node per
-    // sphere, in file order (build decision, SURVEY.md Finding 3).
-    if (const J* sp = prims->find("spheres")) {
-      for (auto& s : sp->arr) {
-        auto h = std::make_shared<Sphere>(jvec3(s, "center", {0, 0, 0}), jvec3(s, "displacement", {0, 0, 0}),
-                                          (float)jnum(s, "radius", 0.5), (uint32_t)jint(s, "material_id", 0));
+    // Legacy schema ({"spheres":[{center,radius,material_id,displacement?}], "quads":[{q,u,v,
+    // material_id}], "boxes":[{a,b,material_id}]}): one scene node per primitive, the groups in file
+    // order, each in array order (build decision, SURVEY.md Finding 3).
+    for (auto& grp : prims->obj) {
+      for (auto& s : grp.second.arr) {
+        const uint32_t mat = (uint32_t)jint(s, "material_id", 0);
+        HPtr h;
+        if (grp.first == "spheres") {
+          h = std::make_shared<Sphere>(jvec3(s, "center", {0, 0, 0}), jvec3(s, "displacement", {0, 0, 0}),
+                                       (float)jnum(s, "radius", 0.5), mat);
+        } else if (grp.first == "quads") {
+          h = std::make_shared<Quad>(jvec3(s, "q", {0, 0, 0}), jvec3(s, "u", {1, 0, 0}), jvec3(s, "v", {0, 0, 1}), mat);
+        } else if (grp.first == "boxes") {
+          h = MakeBox(jvec3(s, "a", {0, 0, 0}), jvec3(s, "b", {1, 1, 1}), mat);
+        } else {
+          err = "legacy primitives: unknown group " + grp.first;
+          return nullptr;
+        }
         list.push_back(h);
         top.push_back(h);
       }

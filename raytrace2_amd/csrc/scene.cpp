@@ -580,15 +580,36 @@ bool LoadScene(const std::string& path, uint64_t seed, Scene& s, std::string& er
 
   const Json* prims = obj.find("primitives");
   if (prims && prims->is_object()) {
-    // Legacy schema: {"spheres": [{center, radius, material_id, displacement?}]}; every sphere is
-    // one top-level scene node in file order (documented adapter, SURVEY.md Finding 3).
+    // Legacy schema (the reference's current loader throws on it, Serialize.cpp:288-290):
+    // {"spheres": [{center, radius, material_id, displacement?}], "quads": [{q, u, v, material_id}],
+    //  "boxes": [{a, b, material_id}]}. Documented adapter (SURVEY.md Finding 3): the groups in the
+    // order the file lists them, each in array order; every primitive is one top-level scene node
+    // (a box is MakeBox's 6-quad list, Quad.hpp:34-50).
     s.legacy_schema = true;
-    if (const Json* sp = prims->find("spheres")) {
-      for (const Json& p : sp->items()) {
-        vec3 c, d;
-        if (!GetVec3(p, "center", {0, 0, 0}, c, err) || !GetVec3(p, "displacement", {0, 0, 0}, d, err))
-          return fail(err);
-        int o = MakeSphere(s, c, d, GetDoubleAsFloat(p, "radius", 0.5), (uint32_t)GetInt(p, "material_id", 0));
+    for (const auto& grp : prims->members()) {
+      const std::string& kind = grp.first;
+      if (kind != "spheres" && kind != "quads" && kind != "boxes")
+        return fail("legacy primitives: unknown group '" + kind + "'");
+      if (!grp.second.is_array()) return fail("legacy primitives: '" + kind + "' must be an array");
+      for (const Json& p : grp.second.items()) {
+        const uint32_t mat = (uint32_t)GetInt(p, "material_id", 0);
+        int o = -1;
+        if (kind == "spheres") {
+          vec3 c, d;
+          if (!GetVec3(p, "center", {0, 0, 0}, c, err) || !GetVec3(p, "displacement", {0, 0, 0}, d, err))
+            return fail(err);
+          o = MakeSphere(s, c, d, GetDoubleAsFloat(p, "radius", 0.5), mat);
+        } else if (kind == "quads") {
+          vec3 q, u, v;
+          if (!GetVec3(p, "q", {0, 0, 0}, q, err) || !GetVec3(p, "u", {1, 0, 0}, u, err) ||
+              !GetVec3(p, "v", {0, 0, 1}, v, err))
+            return fail(err);
+          o = MakeQuad(s, q, u, v, mat);
+        } else {
+          vec3 a, b;
+          if (!GetVec3(p, "a", {0, 0, 0}, a, err) || !GetVec3(p, "b", {1, 1, 1}, b, err)) return fail(err);
+          o = MakeBox(s, a, b, mat);
+        }
         s.primitives.push_back(o);
         s.top.push_back(o);
       }

@@ -23,6 +23,8 @@ CASES = [
     ("checker_test", 64, 48, 64, 8),
     ("perlin_spheres", 64, 48, 64, 8),
     ("cornell_box_scene_graph", 64, 64, 16, 8),
+    ("cornell_box2", 64, 64, 16, 8),  # legacy schema: quads + boxes
+    ("light_scene1", 64, 48, 16, 8),  # legacy schema: spheres + quads, textures
 ]
 
 

@@ -11,7 +11,8 @@ from conftest import SCENES, scene_path
 from oracle.oracle import OracleScene
 
 ALL = ["cornell_box_original", "cornell_box_volume", "final_render_book_1", "book2_final_scene_10000_samples",
-       "checker_test", "perlin_spheres", "cornell_box_scene_graph"]
+       "checker_test", "perlin_spheres", "cornell_box_scene_graph", "cornell_box1", "cornell_box2", "quad_scene1",
+       "light_scene1"]
 
 
 @pytest.mark.parametrize("name", ALL)
@@ -69,6 +70,23 @@ def test_legacy_adapter_camera_and_background():
     assert cam.defocus_angle == pytest.approx(0.6)
     assert s.background_color == (1.0, 1.0, 1.0)  # loader default (Serialize.cpp:204)
     assert s.dims == (0, 0)
+
+
+@pytest.mark.parametrize("name,quads,spheres,top", [("cornell_box1", 6, 0, 6), ("cornell_box2", 18, 0, 8),
+                                                     ("quad_scene1", 5, 0, 5), ("light_scene1", 2, 3, 5)])
+def test_legacy_adapter_quads_and_boxes(name, quads, spheres, top):
+    """Legacy {"primitives": {"spheres"|"quads"|"boxes": [...]}} files (reference data/; its current
+    loader throws on them, Serialize.cpp:288-290): one top-level node per primitive, a box = 6 quads."""
+    i = R.Scene(scene_path(name)).info()
+    assert i.legacy_schema == 1 and (i.quads, i.spheres, i.n_top_nodes) == (quads, spheres, top)
+
+
+def test_legacy_unknown_group_is_an_error(tmp_path):
+    p = tmp_path / "bad.json"
+    p.write_text(json.dumps({"camera": {"center": [0, 0, 1]}, "materials": [{"type": "lambertian"}],
+                             "primitives": {"triangles": [{"material_id": 0}]}}))
+    with pytest.raises(R.Rt2Error, match="triangles"):
+        R.Scene(str(p))
 
 
 def test_write_camera_round_trip_is_byte_identical(tmp_path):
