@@ -62,7 +62,8 @@ constexpr int kBlock = 256;
 #define RT2_EXP_TRACE_TWICE 0  // cost probe: every ray is traced a second time (result discarded)
 #endif
 #ifndef RT2_EXP_TWICE
-#define RT2_EXP_TWICE 0  // cost probes (bits): 1 resolve_hit, 2 rand_unit_vec3, 4 camera_ray run twice
+#define RT2_EXP_TWICE 0  // cost probes (bits): 1 resolve_hit, 2 rand_unit_vec3, 4 camera_ray, 8 slab test,
+                         // 16 quad-run test run twice
 #endif
 #ifndef RT2_EXP_WAVESTEPS
 #define RT2_EXP_WAVESTEPS 0  // diagnostic build: per-wave linear-traversal step counts into diag slots
@@ -72,6 +73,10 @@ constexpr int kBlock = 256;
 #endif
 #ifndef RT2_EXP_ENDTIME
 #define RT2_EXP_ENDTIME 0  // diagnostic build: per-wave start / first-idle / end times (s_memrealtime) into diag
+#endif
+#ifndef RT2_QUAD_PREFETCH
+#define RT2_QUAD_PREFETCH 0  // threaded program: touch the next quad record of a run early (measured slower:
+                             // Cornell 28.1 -> 26.7, book 2 1.45 -> 1.43 Grays/s)
 #endif
 #ifndef RT2_WIDE_PROGRAM
 #define RT2_WIDE_PROGRAM 1  // threaded program: 64-byte steps (entry + first 48 record bytes, one load)
@@ -226,6 +231,13 @@ __device__ __forceinline__ u32x16 sld16(const void* base, uint32_t off) {
   asm("s_load_dwordx16 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(base), "s"(off));
   return v;
 }
+// Software prefetch into the scalar cache: a one-dword load left in flight into `dst`, which stays
+// reserved until sld_wait1(dst) has completed it.
+__device__ __forceinline__ void sld_touch(const void* base, uint32_t off, uint32_t& dst) {
+  off = __builtin_amdgcn_readfirstlane(off);
+  asm volatile("s_load_dword %0, %1, %2" : "=s"(dst) : "s"(base), "s"(off));
+}
+__device__ __forceinline__ void sld_wait1(uint32_t& v) { asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(v)); }
 // 20 dwords (one quad record) at off
 __device__ __forceinline__ void sld20(const void* base, uint32_t off, u32x16& a, u32x4& b) {
   off = __builtin_amdgcn_readfirstlane(off);
@@ -983,6 +995,14 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
           const float4 lo = make_float4(uf(sw[4]), uf(sw[5]), uf(sw[6]), 0.0f);
           const float4 hi = make_float4(uf(sw[8]), uf(sw[9]), uf(sw[10]), 0.0f);
           const bool in = allfin ? aabb_hit_fin(lo, hi, o, inv, tmin, tmax) : aabb_hit(lo, hi, o, inv, tmin, tmax);
+#if RT2_EXP_TWICE & 8
+          {
+            f3 o2 = o;
+            asm volatile("" : "+v"(o2.x), "+v"(o2.y), "+v"(o2.z));
+            const bool in2 = allfin ? aabb_hit_fin(lo, hi, o2, inv, tmin, tmax) : aabb_hit(lo, hi, o2, inv, tmin, tmax);
+            asm volatile("" ::"v"((int)in2));
+          }
+#endif
           next = in ? i + 1u : sw[1];
         }
         i = wave_min_next(next);
@@ -1016,12 +1036,20 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
       // order (issue-bound: one candidate at a time beats two interleaved, measured)
       const uint32_t run = st.w;
       uint32_t codes = st.y;
+#if RT2_WIDE_PROGRAM && RT2_QUAD_PREFETCH
+      // the next record of the run is touched (one scalar load into the scalar cache) while this
+      // quad is tested, so its own load later finds the line on chip
+      uint32_t touch = 0;
+#endif
       for (uint32_t k = 0; k < run; k++, codes >>= 3) {
         const uint32_t o0 = off + 5u * k;
         const uint32_t c0 = codes & 7u;
         float t0;
         bool ok0;
         uint32_t kind0;
+#if RT2_WIDE_PROGRAM && RT2_QUAD_PREFETCH
+        if (k + 1u < run) sld_touch(recs, (o0 + 5u) * 16u, touch);
+#endif
         if (c0 >= 4u) {
 #if RT2_WIDE_PROGRAM
           const u32x8 a = k == 0u ? u32x8{sw[4], sw[5], sw[6], sw[7], sw[8], sw[9], sw[10], sw[11]}
@@ -1046,7 +1074,26 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
           ok0 = quad_cand_u(c0, w0, o, d, inv, t0);
           kind0 = kQuad;
         }
+#if RT2_WIDE_PROGRAM && RT2_QUAD_PREFETCH
+        sld_wait1(touch);
+#endif
         if (kStats) cnt.quad += 1;
+#if RT2_EXP_TWICE & 16
+        {
+          f3 o2 = o;
+          asm volatile("" : "+v"(o2.x), "+v"(o2.y), "+v"(o2.z));
+          float t2 = 0.0f;
+          bool ok2 = false;
+          if (c0 >= 4u) {
+            const u32x8 a = sld8(recs, o0 * 16u);
+            float ra[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) ra[j] = uf(a[j]);
+            ok2 = quad_aa_k(c0 - 4u, ra, o2, d, inv, t2);
+          }
+          asm volatile("" ::"v"(t2), "v"((int)ok2));
+        }
+#endif
         if (ok0 && tmin <= t0 && t0 <= tmax) {
           tmax = t0;
           prim = make_ref(kind0, o0);
