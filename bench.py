@@ -322,8 +322,8 @@ def main():
         R.WriteImage(img / np.float32(a.spp), a.width, a.height, a.out_image)
 
     workload = f"{a.scene} {a.width}x{a.height} @ {a.spp} spp, max_depth {a.max_depth}"
-    if mode == "emulate":
-        partition = f"emulate {a.emulate_world}-way h={a.band_h} rank {me['rank']}"
+    if mode == "emulate":  # the same GPU work as that rank of a real N-GPU run: the same profile key
+        partition = f"{a.emulate_world}-way h={a.band_h} rank {me['rank']}"
     elif n_gpus > 1:
         partition = f"{n_gpus}-way h={a.band_h} rank 0"
     else:
