@@ -84,11 +84,14 @@ constexpr int kBlock = 256;
 #ifndef RT2_RARE_MIN
 #define RT2_RARE_MIN 0  // stack traversal: lanes needed before a rare, expensive step kind runs (0: off)
 #endif
+#ifndef RT2_MIN_WAVES_CORNELL
+#define RT2_MIN_WAVES_CORNELL 7
+#endif
 #ifndef RT2_MIN_WAVES_BOOK1
 #define RT2_MIN_WAVES_BOOK1 8
 #endif
 #ifndef RT2_MIN_WAVES_VOL
-#define RT2_MIN_WAVES_VOL 6
+#define RT2_MIN_WAVES_VOL 7
 #endif
 #ifndef RT2_MIN_WAVES_B2LIN
 #define RT2_MIN_WAVES_B2LIN 7  // book 2 threaded: 3/4/5/6/7/8 waves 934/938/1091/1183/1297/508 Mray/s
@@ -1381,7 +1384,7 @@ constexpr int MinWaves() {
     return RT2_MIN_WAVES_ALL;  // book 2
   if (F == kBook2 && !kStats && kMode == kModeLinear) return RT2_MIN_WAVES_B2LIN;
   if (kStats || kMode != kModeLinear) return 1;
-  if (F == kFeatXform) return 7;                  // Cornell: 72 VGPRs
+  if (F == kFeatXform) return RT2_MIN_WAVES_CORNELL;  // Cornell: 70 VGPRs at 7
   if (F == (kFeatXform | kFeatMedium)) return RT2_MIN_WAVES_VOL;  // Cornell volume: 89 VGPRs at 5
   if (F == kFeatAll) return 1;
   return RT2_MIN_WAVES_BOOK1;                     // book 1
