@@ -15,6 +15,8 @@ spp, frames = (int(sys.argv[4]) if len(sys.argv) > 4 else 1000), int(sys.argv[2]
 sc = R.Scene(scene)
 tr = R.RayTracer(sc, 0)
 tr.SetSamplesPerPixel(spp)
+if len(sys.argv) > 5:
+    tr.max_depth = int(sys.argv[5])
 tr.enable_stats(True)
 tr.OnResize((w, h))
 tr.Render(frames)
@@ -23,7 +25,7 @@ d = st["diag"]
 rays = st["rays"]
 wtrace = max(d[0], 1)
 out = {
-    "scene": scene, "rays": rays,
+    "scene": scene, "max_depth": tr.max_depth, "rays": rays,
     "lane_per_ray": {k: st[k] / rays for k in ("bvh_tests", "quad_tests", "sphere_tests", "xform_visits",
                                                 "medium_tests", "list_visits")},
     "wave_trace_calls": d[0], "active_lanes_per_trace": d[7] / wtrace,
