@@ -91,6 +91,7 @@ struct rt2_tracer {
   size_t sample_budget = size_t(16) << 30;  // bytes; bounds the frames per launch
   int work_split = 16;                     // chunk schedule: work left split into >= k items per lane (0: one chunk)
   int chunk_max = 64;                      // longest chunk (frames)
+  bool chunk_align = true;                 // chunks of >= kOctet frames fill whole sample octets
   uint32_t* d_chunks = nullptr;            // chunk table of the last launch shape (ChunkSchedule)
   size_t chunks_bytes = 0;
   uint32_t n_chunks = 0;
@@ -515,6 +516,7 @@ int rt2_tracer_create(const rt2_scene* s, int device, rt2_tracer** out) {
   if (const char* e = getenv("RT2_FORCE_HYBRID")) t->force_hybrid = e[0] == '1';
   if (const char* e = getenv("RT2_HYBRID_RECORDS")) t->hybrid_cap = atoi(e);
   if (const char* e = getenv("RT2_CHUNK_MAX")) t->chunk_max = std::max(1, atoi(e));
+  if (const char* e = getenv("RT2_CHUNK_ALIGN")) t->chunk_align = e[0] != '0';
   // App.cpp:122-125,157: scene dims when present, else the window default 1600x900
   int w = s->scene.dims_x > 0 && s->scene.dims_y > 0 ? s->scene.dims_x : 1600;
   int h = s->scene.dims_x > 0 && s->scene.dims_y > 0 ? s->scene.dims_y : 900;
@@ -760,7 +762,8 @@ Magic MakeMagic(uint32_t d) {  // rt2_layout.h Magic: floor(n / d) for n < 2^31
 // chunk (each pixel's frames in one item). Cached: the bench repeats one launch shape.
 int ChunkSchedule(rt2_tracer* t, int fb, int n, uint32_t tile_items, int64_t lanes, int sq) {
   const uint64_t key[6] = {(uint64_t)fb, (uint64_t)n, tile_items, (uint64_t)lanes,
-                           (uint64_t)t->work_split | ((uint64_t)t->chunk_max << 32), (uint64_t)sq};
+                           (uint64_t)t->work_split | ((uint64_t)t->chunk_max << 32) | ((uint64_t)t->chunk_align << 63),
+                           (uint64_t)sq};
   if (t->d_chunks && memcmp(key, t->chunk_key, sizeof(key)) == 0) return RT2_OK;
   // items must stay below 2^31 (kernel index arithmetic): shortest chunk that allows it
   const int64_t max_chunks = std::max<int64_t>(1, (int64_t)0x7FFFFFFF / tile_items);
@@ -773,8 +776,9 @@ int ChunkSchedule(rt2_tracer* t, int fb, int n, uint32_t tile_items, int64_t lan
       const double want = (double)(n - s) * (double)tile_items / ((double)t->work_split * (double)lanes);
       len = (int)std::min<double>(want, (double)t->chunk_max);
     }
+    if (t->chunk_align && len >= (int)kOctet) len -= len % (int)kOctet;  // long chunks fill whole sample octets
     len = std::max(len, lo);
-    len = std::min({len, n - s, 0x10000});  // the kernel keeps a chunk's frames left in 16 bits
+    len = std::min({len, n - s, kChunkMaxFrames});
     const uint32_t f = (uint32_t)(fb + s), usq = (uint32_t)sq;
     tab.push_back(f);
     tab.push_back((f % usq) | (((f / usq) % usq) << 16));  // RayTracer.cpp:59-60
@@ -898,11 +902,14 @@ int LaunchFrames(rt2_tracer* t, int n_frames) {
   // frames per launch: the caller's launch_frames, bounded by the sample-buffer budget
   const size_t frame_bytes = (size_t)p.local_pixels * 3 * sizeof(float);
   int per_launch = t->launch_frames > 0 ? std::min(t->launch_frames, n_frames) : n_frames;
-  per_launch = (int)std::max<size_t>(1, std::min<size_t>((size_t)per_launch, t->sample_budget / frame_bytes));
-  size_t need = (size_t)per_launch * frame_bytes;
+  // (the buffer holds whole octets of frames, rt2_layout.h kOctet)
+  const size_t budget_frames = std::max<size_t>(1, t->sample_budget / frame_bytes);
+  per_launch = (int)std::min<size_t>((size_t)per_launch, budget_frames < kOctet ? budget_frames : budget_frames - budget_frames % kOctet);
+  const auto octets = [](size_t frames) { return (frames + kOctet - 1) / kOctet * kOctet; };
+  size_t need = octets((size_t)per_launch) * frame_bytes;
   if (need > t->samples_bytes) {
     // grow geometrically (progressive loops raise their frames per call a little at a time)
-    need = std::max(need, std::min(2 * t->samples_bytes, (t->sample_budget / frame_bytes) * frame_bytes));
+    need = std::max(need, std::min(2 * t->samples_bytes, octets(budget_frames) * frame_bytes));
     HIP_TRY(hipStreamSynchronize(t->stream));  // the old buffer may still be read
     (void)hipFree(t->d_samples);
     t->d_samples = nullptr;

@@ -7,9 +7,10 @@
 // Execution model (MI355X):
 //  * persistent lanes take work items = (pixel, chunk of consecutive frames of the launch); a lane
 //    renders its chunk's frames back to back and writes each frame's sample (float3) to the
-//    per-frame sample buffer; accumulate_kernel then adds a launch's samples to the accumulation in
-//    frame order, so the float sum is the reference's `accumulation_data_[i] += c` sequence
-//    (RayTracer.cpp:64) whatever the chunking;
+//    sample buffer (octets: a pixel's 8 consecutive frames are 96 contiguous bytes, rt2_layout.h);
+//    accumulate_kernel then adds a launch's samples to the accumulation in frame order, so the
+//    float sum is the reference's `accumulation_data_[i] += c` sequence (RayTracer.cpp:64)
+//    whatever the chunking;
 //  * one loop iteration = one bounce for every live lane; a lane whose path ends starts its next
 //    frame in the same iteration (path regeneration), so lanes never idle inside a wave until
 //    their chunk is done;
@@ -101,6 +102,15 @@ constexpr int kBlock = 256;
 #endif
 #ifndef RT2_MIN_WAVES_PER_EU
 #define RT2_MIN_WAVES_PER_EU 0  // 0: per-variant occupancy targets (kMinWaves below)
+#endif
+#ifndef RT2_KARG
+#define RT2_KARG 1  // launch constants re-read from the kernel-argument segment at their uses (see karg16)
+#endif
+#ifndef RT2_KARG_CAMERA
+#define RT2_KARG_CAMERA RT2_KARG
+#endif
+#ifndef RT2_OCTET_STAGE
+#define RT2_OCTET_STAGE 1  // threaded kernels at <= 7 waves: stage a lane's samples in LDS, one 96-B store per octet
 #endif
 
 extern __shared__ float4 s_dyn[];  // [lds_nodes scene records][stack_depth * kBlock stack words]
@@ -250,6 +260,148 @@ __device__ __forceinline__ void sld20(const void* base, uint32_t off, u32x16& a,
 }
 __device__ __forceinline__ float uf(uint32_t u) { return __uint_as_float(u); }
 
+// Launch parameters re-read from the kernel-argument segment where they are used (one scalar load)
+// instead of being held in SGPRs across the render loop: the loop keeps more wave-uniform values
+// live than there are SGPRs, and the compiler's spill of them to VGPR lanes costs one v_readlane (a
+// VALU instruction) per value at every use. Volatile, so the load is not hoisted back out of the
+// loop. The kernel's only argument is its RenderParams, at offset 0 of the segment.
+template <uint32_t kOff>
+__device__ __forceinline__ u32x16 karg16() {
+  static_assert(kOff % 4 == 0, "dword-aligned");
+  u32x16 v;
+  asm volatile("s_load_dwordx16 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)"
+               : "=s"(v)
+               : "s"(__builtin_amdgcn_kernarg_segment_ptr()), "n"(kOff));
+  return v;
+}
+template <uint32_t kOff>
+__device__ __forceinline__ u32x8 karg8() {
+  static_assert(kOff % 4 == 0, "dword-aligned");
+  u32x8 v;
+  asm volatile("s_load_dwordx8 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)"
+               : "=s"(v)
+               : "s"(__builtin_amdgcn_kernarg_segment_ptr()), "n"(kOff));
+  return v;
+}
+
+#define RT2_KOFF(f) ((uint32_t)offsetof(RenderParams, f))
+template <typename T, int k>
+__device__ __forceinline__ T kword(const u32x16& v) {  // a 4- or 8-byte field of a loaded block
+  static_assert(k >= 0 && k + (int)sizeof(T) / 4 <= 16, "field outside the block");
+  // (the element is copied out first: __builtin_bit_cast of a vector-element lvalue reads element 0
+  // with this compiler)
+  if constexpr (sizeof(T) == 4) {
+    const uint32_t x = v[k];
+    return __builtin_bit_cast(T, x);
+  } else {
+    static_assert(sizeof(T) == 8, "field size");
+    const unsigned long long x = (unsigned long long)v[k] | ((unsigned long long)v[k + 1] << 32);
+    return __builtin_bit_cast(T, x);
+  }
+}
+
+// The render loop's launch constants (image, partition, work items, chunk table, magic divisors,
+// seed, sample buffer): two 64-byte blocks and the width, one wait.
+struct LoopArgs {
+  static constexpr uint32_t kA = 144, kB = 212;  // [144, 208) height .. chunks, [212, 276) div_tile_items .. local_pixels
+  static_assert(RT2_KOFF(height) == kA && RT2_KOFF(chunks) + 8 == kA + 64 && RT2_KOFF(div_tile_items) == kB &&
+                    RT2_KOFF(local_pixels) + 4 == kB + 64 &&
+                    RT2_KOFF(width) == kA - 4,
+                "RenderParams layout");
+  u32x16 a, b;
+  uint32_t w;
+  template <typename T, uint32_t kOff>
+  __device__ __forceinline__ T get() const {
+    if constexpr (kOff < kB) {
+      return kword<T, (int)(kOff - kA) / 4>(a);
+    } else {
+      return kword<T, (int)(kOff - kB) / 4>(b);
+    }
+  }
+#define RT2_LA(name, T, f) \
+  __device__ __forceinline__ T name() const { return get<T, RT2_KOFF(f)>(); }
+  RT2_LA(local_rows, int, local_rows)
+  RT2_LA(band_h, int, band_h)
+  RT2_LA(rank, int, rank)
+  RT2_LA(world, int, world)
+  RT2_LA(tile_shift, uint32_t, tile_shift)
+  RT2_LA(tiles_x, int, tiles_x)
+  RT2_LA(tile_items, uint32_t, tile_items)
+  RT2_LA(n_items, uint32_t, n_items)
+  RT2_LA(batch_max, uint32_t, batch_max)
+  RT2_LA(batch_div, uint32_t, batch_div)
+  RT2_LA(frame_begin, int, frame_begin)
+  RT2_LA(max_depth, int, max_depth)
+  RT2_LA(chunks, const uint32_t*, chunks)
+  RT2_LA(div_tile_items, Magic, div_tile_items)
+  RT2_LA(div_tiles_x, Magic, div_tiles_x)
+  RT2_LA(div_band_h, Magic, div_band_h)
+  RT2_LA(div_band_w, Magic, div_band_w)
+  RT2_LA(div_world, Magic, div_world)
+  RT2_LA(samples, float*, samples)
+  RT2_LA(local_pixels, uint32_t, local_pixels)
+#undef RT2_LA
+  __device__ __forceinline__ int width() const { return (int)w; }
+};
+__device__ __forceinline__ LoopArgs loop_args() {
+  LoopArgs r;
+  asm volatile(
+      "s_load_dwordx16 %0, %3, %4\n\ts_load_dwordx16 %1, %3, %5\n\ts_load_dword %2, %3, %6\n\ts_waitcnt lgkmcnt(0)"
+      : "=&s"(r.a), "=&s"(r.b), "=&s"(r.w)
+      : "s"(__builtin_amdgcn_kernarg_segment_ptr()), "n"(LoopArgs::kA), "n"(LoopArgs::kB), "n"(LoopArgs::kA - 4));
+  return r;
+}
+
+// Scene tables used by shading: materials, textures, Perlin vectors and permutations (one load).
+struct ShadeArgs {
+  const float4* materials;
+  const float4* textures;
+  const float4* perlin_vec;
+  const int* perlin_perm;
+};
+__device__ __forceinline__ ShadeArgs shade_args_of(const RenderParams& P) {
+  return ShadeArgs{reinterpret_cast<const float4*>(P.materials), reinterpret_cast<const float4*>(P.textures),
+                   reinterpret_cast<const float4*>(P.perlin_vec), P.perlin_perm};
+}
+__device__ __forceinline__ ShadeArgs shade_args() {
+  static_assert(RT2_KOFF(materials) == 8 && RT2_KOFF(perlin_perm) == 32, "RenderParams layout");
+  const u32x8 v = karg8<8>();
+  auto ptr = [&](int k) { return (unsigned long long)v[k] | ((unsigned long long)v[k + 1] << 32); };
+  return ShadeArgs{reinterpret_cast<const float4*>(ptr(0)), reinterpret_cast<const float4*>(ptr(2)),
+                   reinterpret_cast<const float4*>(ptr(4)), reinterpret_cast<const int*>(ptr(6))};
+}
+
+// The same launch constants read from the kernel argument as the compiler sees fit (RT2_KARG 0).
+__device__ __forceinline__ LoopArgs loop_args_of(const RenderParams& P) {
+  LoopArgs r;
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(&P);
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    r.a[k] = w[LoopArgs::kA / 4 + k];
+    r.b[k] = w[LoopArgs::kB / 4 + k];
+  }
+  r.w = (uint32_t)P.width;
+  return r;
+}
+#if RT2_KARG
+#define RT2_LOOP_ARGS() loop_args()
+#define RT2_SHADE_ARGS() shade_args()
+#else
+#define RT2_LOOP_ARGS() loop_args_of(P)
+#define RT2_SHADE_ARGS() shade_args_of(P)
+#endif
+
+// Philox keys and the image width (the stream's pixel index), one wait.
+__device__ __forceinline__ void seed_args(uint32_t& k0, uint32_t& k1, uint32_t& width) {
+  static_assert(RT2_KOFF(seed_hi) == RT2_KOFF(seed_lo) + 4, "RenderParams layout");
+  unsigned long long k;
+  asm volatile("s_load_dwordx2 %0, %2, %3\n\ts_load_dword %1, %2, %4\n\ts_waitcnt lgkmcnt(0)"
+               : "=&s"(k), "=&s"(width)
+               : "s"(__builtin_amdgcn_kernarg_segment_ptr()), "n"(RT2_KOFF(seed_lo)), "n"(RT2_KOFF(width)));
+  k0 = (uint32_t)k;
+  k1 = (uint32_t)(k >> 32);
+}
+
 // ------------------------------------------------------------------------------------------
 // Philox4x32-10 path stream keyed by (seed, pixel, frame). Draws are taken in groups of K <= 4
 // consecutive values; `n` counts draws and the buffer holds the block of the last value drawn
@@ -310,7 +462,13 @@ struct Path {
 #pragma unroll
     for (int j = 0; j < K; j++) v[j] = sel4((i + (uint32_t)j) & 3u, r0, r1, r2, r3);
     if (fresh || i + (uint32_t)K > 4u) {
+#if RT2_KARG
+      uint32_t key0, key1, w;
+      seed_args(key0, key1, w);  // re-read at the refill (see karg16)
+      philox(key0, key1, (xy >> 16) * w + (xy & 0xFFFFu), frame, (n >> 2) + (fresh ? 0u : 1u), r0, r1, r2, r3);
+#else
       philox(k0, k1, (xy >> 16) * width + (xy & 0xFFFFu), frame, (n >> 2) + (fresh ? 0u : 1u), r0, r1, r2, r3);
+#endif
 #pragma unroll
       for (int j = 0; j < K; j++)
         if (fresh || i + (uint32_t)j >= 4u) v[j] = sel4((i + (uint32_t)j) & 3u, r0, r1, r2, r3);
@@ -1256,9 +1414,9 @@ __device__ __forceinline__ void resolve_hit(const Nodes<kMode>& N, const HitRef&
 
 // ------------------------------------------------------------------------------------------
 // Textures (Texture.cpp:7-22, PerlinNoiseGen.cpp:10-88)
-__device__ __forceinline__ float perlin_noise(const RenderParams& P, uint32_t voff, uint32_t poff, uint32_t pc, f3 p) {
-  const float4* V = reinterpret_cast<const float4*>(P.perlin_vec) + voff;
-  const int* Px = P.perlin_perm + poff;
+__device__ __forceinline__ float perlin_noise(const ShadeArgs& S, uint32_t voff, uint32_t poff, uint32_t pc, f3 p) {
+  const float4* V = S.perlin_vec + voff;
+  const int* Px = S.perlin_perm + poff;
   const int* Py = Px + pc;
   const int* Pz = Py + pc;
   float fx = floorf(p.x), fy = floorf(p.y), fz = floorf(p.z);
@@ -1283,8 +1441,8 @@ __device__ __forceinline__ float perlin_noise(const RenderParams& P, uint32_t vo
 }
 
 template <uint32_t F>
-__device__ __forceinline__ f3 tex_value(const RenderParams& P, uint32_t idx, f3 p) {
-  const float4* T = reinterpret_cast<const float4*>(P.textures);
+__device__ __forceinline__ f3 tex_value(const ShadeArgs& S, uint32_t idx, f3 p) {
+  const float4* T = S.textures;
   for (int guard = 0; guard < 32; guard++) {
     float4 t0 = T[3 * idx];
     uint32_t type = bits(t0.x);
@@ -1306,14 +1464,14 @@ __device__ __forceinline__ f3 tex_value(const RenderParams& P, uint32_t idx, f3 
         float acc = 0.0f, weight = 1.0f;
         f3 tp = p;
         for (int k = 0; k < 7; k++) {
-          acc += weight * perlin_noise(P, voff, poff, pc, tp);
+          acc += weight * perlin_noise(S, voff, poff, pc, tp);
           weight *= 0.5f;
           tp = tp * 2.0f;
         }
         float arg = t1.x * p.z + 10.0f * fabsf(acc);
         return alb * (1.0f + (float)sin((double)arg));
       }
-      return alb * (1.0f + perlin_noise(P, voff, poff, pc, t1.x * p));
+      return alb * (1.0f + perlin_noise(S, voff, poff, pc, t1.x * p));
     }
     break;
   }
@@ -1333,13 +1491,27 @@ __device__ __forceinline__ void camera_ray(const RenderParams& P, Path& g, f3& o
   } else {
     g.take<3>(u);  // px, py, time
   }
-  float px = ((float)s_i + u[0]) * C.recip_sqrt_spp - 0.5f;
-  float py = ((float)s_j + u[1]) * C.recip_sqrt_spp - 0.5f;
+#if RT2_KARG_CAMERA
+  // pixel00, du, dv, center (words 0-11) and recip_sqrt_spp (word 19) from the argument segment
+  constexpr uint32_t kCam = (uint32_t)offsetof(RenderParams, cam);
+  static_assert(offsetof(CameraParams, recip_sqrt_spp) == 19 * 4, "CameraParams layout");
+  const u32x16 ca = karg16<kCam>();
+  const u32x8 cb = karg8<kCam + 48u>();  // words 12-19
+  const float rs = uf(cb[7]);
+  f3 p00 = mk(uf(ca[0]), uf(ca[1]), uf(ca[2]));
+  f3 du = mk(uf(ca[3]), uf(ca[4]), uf(ca[5]));
+  f3 dv = mk(uf(ca[6]), uf(ca[7]), uf(ca[8]));
+  f3 c = mk(uf(ca[9]), uf(ca[10]), uf(ca[11]));
+#else
+  const float rs = C.recip_sqrt_spp;
   f3 p00 = mk(C.pixel00[0], C.pixel00[1], C.pixel00[2]);
   f3 du = mk(C.du[0], C.du[1], C.du[2]);
   f3 dv = mk(C.dv[0], C.dv[1], C.dv[2]);
-  f3 pc = (p00 + (((float)x + px) * du)) + (((float)y + py) * dv);
   f3 c = mk(C.center[0], C.center[1], C.center[2]);
+#endif
+  float px = ((float)s_i + u[0]) * rs - 0.5f;
+  float py = ((float)s_j + u[1]) * rs - 0.5f;
+  f3 pc = (p00 + (((float)x + px) * du)) + (((float)y + py) * dv);
   if constexpr (Has<F, kFeatDefocus>()) {
     if (defocus) {
       // RandInUnitDisk (uniform in the unit disk) by the inverse-CDF map r = sqrt(u), phi = 2 pi v
@@ -1362,14 +1534,14 @@ __device__ __forceinline__ void camera_ray(const RenderParams& P, Path& g, f3& o
 // Local (row-band) pixel index of global pixel xy: global row y lies in band y / band_h of period
 // y / (band_h * world) and is stored as local row (y / (band_h * world)) * band_h + y % band_h
 // (rt2_layout.h BandRank).
-__device__ __forceinline__ uint32_t local_index(const RenderParams& P, uint32_t xy) {
+__device__ __forceinline__ uint32_t local_index(const LoopArgs& A, uint32_t xy) {
   const uint32_t x = xy & 0xFFFFu, y = xy >> 16;
   uint32_t r = y;
-  if (P.world > 1) {
-    const uint32_t bh = (uint32_t)P.band_h;
-    r = udiv(y, P.div_band_w) * bh + (y - udiv(y, P.div_band_h) * bh);
+  if (A.world() > 1) {
+    const uint32_t bh = (uint32_t)A.band_h();
+    r = udiv(y, A.div_band_w()) * bh + (y - udiv(y, A.div_band_h()) * bh);
   }
-  return r * (uint32_t)P.width + x;
+  return r * (uint32_t)A.width() + x;
 }
 
 // Occupancy target (waves per SIMD the register allocation must allow), chosen per variant by
@@ -1390,9 +1562,20 @@ constexpr int MinWaves() {
   return RT2_MIN_WAVES_BOOK1;                     // book 1
 }
 
+// Sample octets staged in LDS (rt2_layout.h kOctet): a lane keeps the first 7 samples of an octet in
+// LDS planes and writes the whole octet (96 B, three full 32-B sectors) with six 16-B stores when
+// the 8th is done; a chunk edge inside an octet writes its samples one by one. 5.25 KB per wave:
+// the threaded kernels at <= 7 waves per SIMD (147 KB per CU); other kernels store directly.
+template <uint32_t F, int kMode, bool kStats>
+constexpr bool OctetStaged() {
+  return RT2_OCTET_STAGE && kMode == kModeLinear && !kStats && MinWaves<F, kMode, kStats>() <= 7;
+}
+constexpr uint32_t kOctPlanes = 3u * (kOctet - 1u);  // [slot][component] planes of 64 lanes
+
 template <uint32_t F, int kMode, bool kStats>
 __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render_kernel(const RenderParams P) {
   constexpr bool kLds = kMode == kModeStackLds || kMode == kModeStackHybrid;
+  constexpr bool kOct = OctetStaged<F, kMode, kStats>();
   Nodes<kMode> N{reinterpret_cast<const float4*>(P.nodes), P.lds_nodes};
   if constexpr (kLds) {
     const float4* src = reinterpret_cast<const float4*>(P.nodes);
@@ -1401,7 +1584,11 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
   }
   uint32_t* stk = reinterpret_cast<uint32_t*>(s_dyn + (kLds ? P.lds_nodes : 0u)) + threadIdx.x;
   const int lane = (int)__lane_id();
-  const float4* M = reinterpret_cast<const float4*>(P.materials);
+  float* oct_wave = nullptr;  // this wave's staging planes (wave-uniform; lanes add their id)
+  if constexpr (kOct) {
+    __shared__ float s_oct[(kBlock / 64) * kOctPlanes * 64];
+    oct_wave = s_oct + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * (kOctPlanes * 64u);
+  }
   const f3 bg = mk(P.background[0], P.background[1], P.background[2]);
   bool need = true;   // lane wants a work item
   bool idle = false;  // no work left for this lane: it stays in the loop, masked, until the wave ends,
@@ -1418,9 +1605,9 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
   path.r0 = path.r1 = path.r2 = path.r3 = 0;
   f3 ro = mk(0, 0, 0), rd = mk(0, 0, 1), thr = mk(1, 1, 1);
   float rtime = 0.0f;
-  // depth_left (RayColor's depth, low 16 bits) | frames of the lane's chunk after this one (high 16)
+  // depth_left (RayColor's depth, bits 0-15) | frames of the lane's chunk after this one (bits 16-28)
+  // | the first octet slot this lane holds in the current octet (bits 29-31)
   uint32_t dl = 0;
-  const uint32_t max_depth = (uint32_t)P.max_depth;  // <= 0xFFFF (rt2_tracer_set_max_depth)
   Counters cnt = {};
   bool overflow = false;
 #if RT2_EXP_ENDTIME
@@ -1451,6 +1638,8 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
     // items still spread over all waves.
     unsigned long long mask = __ballot(need && !idle);
     if (mask != 0ull) {
+      const LoopArgs A = RT2_LOOP_ARGS();
+      const uint32_t max_depth = (uint32_t)A.max_depth();  // <= 0xFFFF (rt2_tracer_set_max_depth)
       const uint32_t count = (uint32_t)__popcll(mask);
       const uint32_t avail = bend - bnext;
       const uint32_t old = bnext;
@@ -1458,8 +1647,8 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
       if (count > avail) {
         const uint32_t want = count - avail;
         // work left as of this wave's last reservation (stale, so an overestimate)
-        const uint32_t left = P.n_items > bend ? P.n_items - bend : 0u;
-        const uint32_t size = max(want, min(P.batch_max, left / P.batch_div));
+        const uint32_t left = A.n_items() > bend ? A.n_items() - bend : 0u;
+        const uint32_t size = max(want, min(A.batch_max(), left / A.batch_div()));
         uint32_t b = 0;
         if (lane == __builtin_amdgcn_readfirstlane(lane)) b = atomicAdd(P.work_counter, size);
         fresh = __builtin_amdgcn_readfirstlane(b);
@@ -1472,29 +1661,31 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
         const uint32_t k = (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
         const uint32_t item = k < avail ? old + k : fresh + (k - avail);
         // (no `continue` here: every lane reaches the loop-head ballots below)
-        if (item >= P.n_items) {
+        if (item >= A.n_items()) {
           idle = true;  // no work left for this lane
         } else {
-          const uint32_t chunk = udiv(item, P.div_tile_items);  // chunk-major: every tile's chunk 0 first
-          const uint32_t titem = item - chunk * P.tile_items;
+          const uint32_t chunk = udiv(item, A.div_tile_items());  // chunk-major: every tile's chunk 0 first
+          const uint32_t titem = item - chunk * A.tile_items();
           const uint32_t tile = titem >> 6, within = titem & 63u;
-          const uint32_t trow = udiv(tile, P.div_tiles_x);
+          const uint32_t trow = udiv(tile, A.div_tiles_x());
           // tiles of (64 >> tile_shift) local rows x (1 << tile_shift) pixels
-          const uint32_t tw = 1u << P.tile_shift;
-          const int x = (int)((tile - trow * (uint32_t)P.tiles_x) * tw + (within & (tw - 1u)));
-          const int r = (int)(trow * (64u >> P.tile_shift) + (within >> P.tile_shift));
+          const uint32_t tsh = A.tile_shift(), tw = 1u << tsh;
+          const int x = (int)((tile - trow * (uint32_t)A.tiles_x()) * tw + (within & (tw - 1u)));
+          const int r = (int)(trow * (64u >> tsh) + (within >> tsh));
           // the chunk's first frame and its stratum (RayTracer.cpp:59-60, from the host's table),
-          // and the next chunk's first frame (<= first + 0x10000)
-          const uint32_t* ce = P.chunks + 2u * chunk;
+          // and the next chunk's first frame (<= first + kChunkMaxFrames)
+          const uint32_t* ce = A.chunks() + 2u * chunk;
           const int f = (int)ce[0];
           const int fstop = (int)ce[2];
-          if (x < P.width && r < P.local_rows) {  // else: a lane of a partial edge tile
+          if (x < A.width() && r < A.local_rows()) {  // else: a lane of a partial edge tile
             uint32_t y = (uint32_t)r;
-            if (P.world > 1) {  // local row -> global row (rt2_layout.h BandRank)
-              const uint32_t per = udiv((uint32_t)r, P.div_band_h);  // the rank's band in period `per`
-              const uint32_t pm = per - udiv(per, P.div_world) * (uint32_t)P.world;
-              const uint32_t phase = (uint32_t)P.rank >= pm ? (uint32_t)P.rank - pm : (uint32_t)P.rank + (uint32_t)P.world - pm;
-              y = (per * (uint32_t)P.world + phase) * (uint32_t)P.band_h + ((uint32_t)r - per * (uint32_t)P.band_h);
+            const uint32_t world = (uint32_t)A.world();
+            if (world > 1u) {  // local row -> global row (rt2_layout.h BandRank)
+              const uint32_t bh = (uint32_t)A.band_h(), rank = (uint32_t)A.rank();
+              const uint32_t per = udiv((uint32_t)r, A.div_band_h());  // the rank's band in period `per`
+              const uint32_t pm = per - udiv(per, A.div_world()) * world;
+              const uint32_t phase = rank >= pm ? rank - pm : rank + world - pm;
+              y = (per * world + phase) * bh + ((uint32_t)r - per * bh);
             }
             path.xy = (uint32_t)x | (y << 16);
             item_rays = 0;
@@ -1503,7 +1694,7 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
             path.sij = ce[1];  // then advanced per frame below
             camera_ray<F>(P, path, ro, rd, rtime);
             thr = mk(1, 1, 1);
-            dl = max_depth | ((uint32_t)(fstop - f - 1) << 16);
+            dl = max_depth | ((uint32_t)(fstop - f - 1) << 16) | (((uint32_t)(f - A.frame_begin()) & (kOctet - 1u)) << 29);
           }
         }
       }
@@ -1566,10 +1757,11 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
         } else {
           resolve_hit<F>(N, h, ro, rd, rtime, hp, hn, front, mat);
         }
-        float4 m0 = M[2 * mat], m1 = M[2 * mat + 1];
+        const ShadeArgs S = RT2_SHADE_ARGS();
+        float4 m0 = S.materials[2 * mat], m1 = S.materials[2 * mat + 1];
         uint32_t type = bits(m0.x);
         if (type == kMatDiffuseLight) {
-          color = thr * tex_value<F>(P, bits(m1.z), hp);
+          color = thr * tex_value<F>(S, bits(m1.z), hp);
           done = true;
         } else {
           f3 att, dir;
@@ -1606,11 +1798,11 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
             dir = refl ? reflect(ud, hn) : refract(ud, hn, ri);
           } else if (Has<F, kFeatMedium>() && type == kMatIsotropic) {
             dir = ru;
-            att = tex_value<F>(P, bits(m1.z), hp);
+            att = tex_value<F>(S, bits(m1.z), hp);
           } else {  // Lambertian / Texture
             dir = hn + ru;
             if (near_zero(dir)) dir = hn;
-            att = (type == kMatLambertian) ? mk(m0.y, m0.z, m0.w) : tex_value<F>(P, bits(m1.z), hp);
+            att = (type == kMatLambertian) ? mk(m0.y, m0.z, m0.w) : tex_value<F>(S, bits(m1.z), hp);
           }
           thr = thr * att;
           ro = hp;
@@ -1622,13 +1814,45 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
     RT2_STAMP(st_shade);
     if (done) {
       // this frame's sample, summed in frame order by accumulate_kernel (RayTracer.cpp:64)
-      const uint32_t lidx = local_index(P, path.xy);
-      float* sp = P.samples + 3ull * ((unsigned long long)((int)path.frame - P.frame_begin) * P.local_pixels + lidx);
-      sp[0] = color.x;
-      sp[1] = color.y;
-      sp[2] = color.z;
+      const LoopArgs A = RT2_LOOP_ARGS();
+      const uint32_t lidx = local_index(A, path.xy);
+      const uint32_t fr = path.frame - (uint32_t)A.frame_begin();  // launch-relative frame
+      const uint32_t slot = fr & (kOctet - 1u);
+      float* blk = A.samples() + 3ull * kOctet * ((unsigned long long)(fr / kOctet) * A.local_pixels() + lidx);
+      const bool more = ((dl >> 16) & kChunkLeftMask) != 0u;  // frames of the chunk after this one
+      if constexpr (kOct) {
+        float* oct = oct_wave + __lane_id();
+        if (slot == kOctet - 1u || !more) {
+          const uint32_t first = dl >> 29;
+          if (first == 0u && slot == kOctet - 1u) {  // the whole octet: six 16-B stores
+            float4* b4 = reinterpret_cast<float4*>(blk);
+#pragma unroll
+            for (uint32_t j = 0; j < 5; j++)  // planes 4j..4j+3 (one 16-B store each, few live registers)
+              b4[j] = make_float4(oct[64u * (4u * j)], oct[64u * (4u * j + 1u)], oct[64u * (4u * j + 2u)],
+                                  oct[64u * (4u * j + 3u)]);
+            b4[5] = make_float4(oct[64u * 20u], color.x, color.y, color.z);
+          } else {  // a chunk edge inside the octet: this lane's slots first..slot
+            for (uint32_t k = first; k < slot; k++) {
+              blk[3u * k] = oct[64u * (3u * k)];
+              blk[3u * k + 1u] = oct[64u * (3u * k + 1u)];
+              blk[3u * k + 2u] = oct[64u * (3u * k + 2u)];
+            }
+            blk[3u * slot] = color.x;
+            blk[3u * slot + 1u] = color.y;
+            blk[3u * slot + 2u] = color.z;
+          }
+        } else {
+          oct[64u * (3u * slot)] = color.x;
+          oct[64u * (3u * slot + 1u)] = color.y;
+          oct[64u * (3u * slot + 2u)] = color.z;
+        }
+      } else {
+        blk[3u * slot] = color.x;
+        blk[3u * slot + 1u] = color.y;
+        blk[3u * slot + 2u] = color.z;
+      }
       int f = (int)path.frame + 1;
-      if (dl >> 16) {
+      if (more) {
         path.start((uint32_t)f);
         {  // next stratum: (f % sq, f / sq % sq) from the previous frame's
           const uint32_t sq = (uint32_t)P.cam.sqrt_spp;
@@ -1651,7 +1875,8 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
 #endif
         camera_ray<F>(P, path, ro, rd, rtime);
         thr = mk(1, 1, 1);
-        dl = ((dl & 0xFFFF0000u) - 0x10000u) | max_depth;
+        // one frame fewer left; after the octet's last slot the next octet starts at slot 0
+        dl = (((dl & 0x1FFF0000u) - 0x10000u) | (uint32_t)A.max_depth()) | (slot == kOctet - 1u ? 0u : (dl & 0xE0000000u));
       } else {
         if (kStats && P.ray_counts) atomicAdd(P.ray_counts + lidx, item_rays);
         need = true;
@@ -1700,38 +1925,33 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
 // ------------------------------------------------------------------------------------------
 // RayTracer.cpp:64-66 for a launch's frames: accum[i] += sample(f) in frame order (the float sum
 // of the reference's per-Update accumulation, bit for bit), then the live display value
-// pixels[i] = ToColor(clamp(accum[i] / frame_idx, 0, 1)). One thread per local pixel; a frame's
-// samples are pixel-contiguous, so every load is coalesced and the kernel streams the sample
-// buffer once at HBM rate.
+// pixels[i] = ToColor(clamp(accum[i] / frame_idx, 0, 1)). One thread per local pixel reading its
+// octets (96 contiguous bytes, six 16-B loads; neighbouring threads' octets are adjacent), so the
+// kernel streams the sample buffer once at HBM rate.
 __global__ __launch_bounds__(256) void accumulate_kernel(const float* __restrict__ samples, float* __restrict__ accum,
                                                          uint32_t* __restrict__ pixels, uint32_t npix, int n_frames,
                                                          int frame_idx) {
   const uint32_t i = blockIdx.x * 256u + threadIdx.x;
   if (i >= npix) return;
   float a0 = accum[3 * i], a1 = accum[3 * i + 1], a2 = accum[3 * i + 2];
-  const float* s = samples + 3ull * i;
-  const unsigned long long stride = 3ull * npix;
-  int f = 0;
-  for (; f + 4 <= n_frames; f += 4) {  // four frames' loads in flight, summed in order
-    float x[4][3];
+  const float4* s = reinterpret_cast<const float4*>(samples) + 6ull * i;
+  const unsigned long long stride = 6ull * npix;  // float4s per octet plane
+  for (int f = 0; f < n_frames; f += (int)kOctet, s += stride) {
+    float x[3 * kOctet];
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-      x[k][0] = s[k * stride];
-      x[k][1] = s[k * stride + 1];
-      x[k][2] = s[k * stride + 2];
+    for (int j = 0; j < 6; j++) {
+      const float4 q = s[j];
+      x[4 * j] = q.x, x[4 * j + 1] = q.y, x[4 * j + 2] = q.z, x[4 * j + 3] = q.w;
     }
+    const int m = n_frames - f < (int)kOctet ? n_frames - f : (int)kOctet;  // frames of this octet
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-      a0 += x[k][0];
-      a1 += x[k][1];
-      a2 += x[k][2];
+    for (int k = 0; k < (int)kOctet; k++) {
+      if (k < m) {
+        a0 += x[3 * k];
+        a1 += x[3 * k + 1];
+        a2 += x[3 * k + 2];
+      }
     }
-    s += 4 * stride;
-  }
-  for (; f < n_frames; f++, s += stride) {
-    a0 += s[0];
-    a1 += s[1];
-    a2 += s[2];
   }
   accum[3 * i] = a0;
   accum[3 * i + 1] = a1;

@@ -162,6 +162,17 @@ struct Magic {
   uint32_t m, s;
 };
 
+// Sample buffer: a launch's frames in octets of kOctet consecutive frames (launch-relative frame
+// fr: octet fr / kOctet, slot fr % kOctet); a pixel's octet is 3 * kOctet floats (96 bytes)
+// contiguous, pixels adjacent within an octet plane: float index
+// ((fr / kOctet) * local_pixels + pixel) * 3 * kOctet + 3 * (fr % kOctet) + component.
+// A lane writes a whole octet at once (three full 32-B sectors) instead of 12 B at a time.
+constexpr uint32_t kOctet = 8;
+// Frame chunks hold at most kChunkMaxFrames frames: the kernel keeps a chunk's frames left in
+// 13 bits of a register that also holds the ray depth and the lane's first octet slot.
+constexpr int kChunkMaxFrames = 0x2000;
+constexpr uint32_t kChunkLeftMask = 0x1FFFu;
+
 struct RenderParams {
   const void* nodes;      // float4[]
   const void* materials;  // float4[]
@@ -190,7 +201,7 @@ struct RenderParams {
   Magic div_tile_items, div_tiles_x;  // item -> (chunk, tile), tile -> tile row
   Magic div_band_h, div_band_w, div_world;  // band_h, band_h * world, world (row-band partition)
   uint32_t seed_lo, seed_hi;
-  float* samples;          // float3 per (launch frame, local pixel): [n_frames][local pixels][3]
+  float* samples;          // float3 per (launch frame, local pixel) in octets (kOctet above)
   uint32_t local_pixels;   // width * local_rows
   uint32_t* ray_counts;    // optional: += rays per local pixel (atomic: chunks of a pixel overlap)
   uint32_t* work_counter;  // zeroed before launch
