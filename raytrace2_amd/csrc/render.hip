@@ -86,13 +86,13 @@ constexpr int kBlock = 256;
 #define RT2_RARE_MIN 0  // stack traversal: lanes needed before a rare, expensive step kind runs (0: off)
 #endif
 #ifndef RT2_MIN_WAVES_CORNELL
-#define RT2_MIN_WAVES_CORNELL 7
+#define RT2_MIN_WAVES_CORNELL 8
 #endif
 #ifndef RT2_MIN_WAVES_BOOK1
 #define RT2_MIN_WAVES_BOOK1 8
 #endif
 #ifndef RT2_MIN_WAVES_VOL
-#define RT2_MIN_WAVES_VOL 7
+#define RT2_MIN_WAVES_VOL 8
 #endif
 #ifndef RT2_MIN_WAVES_B2LIN
 #define RT2_MIN_WAVES_B2LIN 7  // book 2 threaded: 3/4/5/6/7/8 waves 934/938/1091/1183/1297/508 Mray/s
@@ -108,6 +108,9 @@ constexpr int kBlock = 256;
 #endif
 #ifndef RT2_KARG_CAMERA
 #define RT2_KARG_CAMERA RT2_KARG
+#endif
+#ifndef RT2_LDS_RNG
+#define RT2_LDS_RNG 1  // threaded kernels: the lane's Philox block in LDS rather than live VGPRs
 #endif
 #ifndef RT2_OCTET_STAGE
 #define RT2_OCTET_STAGE 1  // threaded kernels at <= 7 waves: stage a lane's samples in LDS, one 96-B store per octet
@@ -441,17 +444,30 @@ __device__ __forceinline__ uint32_t sel4(uint32_t i, uint32_t r0, uint32_t r1, u
 }
 __device__ __forceinline__ float to_unit(uint32_t v) { return (float)(v >> 8) * (1.0f / 16777216.0f); }
 
-// The per-lane path context the samplers need.
-struct Path {
+// The per-lane path context the samplers need. kLdsRng: the lane's current Philox block lives in
+// LDS planes (word k of the lane at rbw[64 k + lane]; rbw is the wave's base, wave-uniform) instead
+// of four VGPRs that stay live across the whole render loop.
+template <bool kLdsRng>
+struct PathT {
   uint32_t k0, k1, width;  // wave-uniform: seed, image width
   uint32_t frame;
   uint32_t xy;   // pixel x | y << 16 (global image coordinates)
   uint32_t sij;  // stratum s_i | s_j << 16 of `frame` (RayTracer.cpp:59-60), advanced per frame
   uint32_t n;
-  uint32_t r0, r1, r2, r3;
+  uint32_t r0, r1, r2, r3;  // the block (kLdsRng false)
+  uint32_t* rbw;            // the wave's LDS planes (kLdsRng true)
   __device__ __forceinline__ void start(uint32_t f) {
     frame = f;
     n = 0;  // buffer holds block -1: the first group refills
+  }
+  __device__ __forceinline__ void block(uint32_t b, uint32_t& w0, uint32_t& w1, uint32_t& w2, uint32_t& w3) const {
+#if RT2_KARG
+    uint32_t key0, key1, w;
+    seed_args(key0, key1, w);  // re-read at the refill (see karg16)
+    philox(key0, key1, (xy >> 16) * w + (xy & 0xFFFFu), frame, b, w0, w1, w2, w3);
+#else
+    philox(k0, k1, (xy >> 16) * width + (xy & 0xFFFFu), frame, b, w0, w1, w2, w3);
+#endif
   }
   // K consecutive uniforms in [0,1) (24-bit mantissa), in stream order
   template <int K>
@@ -459,19 +475,30 @@ struct Path {
     uint32_t i = n & 3u;
     bool fresh = i == 0u;
     uint32_t v[K];
+    if constexpr (kLdsRng) {
+      uint32_t* rb = rbw + __lane_id();
 #pragma unroll
-    for (int j = 0; j < K; j++) v[j] = sel4((i + (uint32_t)j) & 3u, r0, r1, r2, r3);
-    if (fresh || i + (uint32_t)K > 4u) {
-#if RT2_KARG
-      uint32_t key0, key1, w;
-      seed_args(key0, key1, w);  // re-read at the refill (see karg16)
-      philox(key0, key1, (xy >> 16) * w + (xy & 0xFFFFu), frame, (n >> 2) + (fresh ? 0u : 1u), r0, r1, r2, r3);
-#else
-      philox(k0, k1, (xy >> 16) * width + (xy & 0xFFFFu), frame, (n >> 2) + (fresh ? 0u : 1u), r0, r1, r2, r3);
-#endif
+      for (int j = 0; j < K; j++) v[j] = rb[64u * ((i + (uint32_t)j) & 3u)];
+      if (fresh || i + (uint32_t)K > 4u) {
+        uint32_t w0, w1, w2, w3;
+        block((n >> 2) + (fresh ? 0u : 1u), w0, w1, w2, w3);
 #pragma unroll
-      for (int j = 0; j < K; j++)
-        if (fresh || i + (uint32_t)j >= 4u) v[j] = sel4((i + (uint32_t)j) & 3u, r0, r1, r2, r3);
+        for (int j = 0; j < K; j++)
+          if (fresh || i + (uint32_t)j >= 4u) v[j] = sel4((i + (uint32_t)j) & 3u, w0, w1, w2, w3);
+        rb[0] = w0;
+        rb[64] = w1;
+        rb[128] = w2;
+        rb[192] = w3;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < K; j++) v[j] = sel4((i + (uint32_t)j) & 3u, r0, r1, r2, r3);
+      if (fresh || i + (uint32_t)K > 4u) {
+        block((n >> 2) + (fresh ? 0u : 1u), r0, r1, r2, r3);
+#pragma unroll
+        for (int j = 0; j < K; j++)
+          if (fresh || i + (uint32_t)j >= 4u) v[j] = sel4((i + (uint32_t)j) & 3u, r0, r1, r2, r3);
+      }
     }
     n += (uint32_t)K;
 #pragma unroll
@@ -506,9 +533,10 @@ __device__ __forceinline__ void cos_sin_2pi(float v, float& c, float& s) {
 // Math.hpp:26-43 RandUnitVec3 (uniform on the unit sphere) by the inverse-CDF map z = 1 - 2u,
 // phi = 2 pi v: two uniforms and no rejection loop, so a wave never waits on its unluckiest
 // lane's retries (the oracle draws the same map; DESIGN.md "Sampling").
-__device__ __forceinline__ f3 rand_unit_vec3(Path& g) {
+template <class G>
+__device__ __forceinline__ f3 rand_unit_vec3(G& g) {
   float u[2];
-  g.take<2>(u);
+  g.template take<2>(u);
   const float z = 1.0f - 2.0f * u[0];
   const float r = sqrtf(1.0f - z * z);
   float c, s;
@@ -820,9 +848,9 @@ __device__ __forceinline__ void ray_in_space(const Nodes<kMode>& N, uint32_t xre
 
 // ConstantMedium::Hit (ConstantMedium.cpp:14-58) on [tmin, tmax]: two boundary queries, then one
 // random number for the free-flight distance. Returns the medium's t.
-template <uint32_t F, int kMode>
+template <uint32_t F, int kMode, class G>
 __device__ __forceinline__ bool medium_t(const Nodes<kMode>& N, uint32_t off, f3 o, f3 d, float time, float tmin,
-                                         float tmax, Path& path, float& t_out, Counters& cnt) {
+                                         float tmax, G& path, float& t_out, Counters& cnt) {
   float4 r0 = N[off];
   uint32_t bref = bits(r0.z);
   float t1, t2;
@@ -896,9 +924,9 @@ __device__ __forceinline__ bool boundary_t_lin(const void* recs, uint32_t ref, f
 }
 
 // medium_t with the boundary queries above (same operations, same random draw)
-template <uint32_t F>
+template <uint32_t F, class G>
 __device__ __forceinline__ bool medium_t_lin(const void* recs, const u32x4 r0, f3 o, f3 d, float time, float tmin,
-                                             float tmax, Path& path, float& t_out, Counters& cnt) {
+                                             float tmax, G& path, float& t_out, Counters& cnt) {
   const uint32_t bref = r0.z;
   float t1, t2;
   if (!boundary_t_lin<F>(recs, bref, o, d, time, -FLT_MAX, FLT_MAX, t1, cnt)) return false;
@@ -929,9 +957,9 @@ struct HitRef {
 
 // Stack traversal (any scene): each lane walks its own steps — LDS stack pops, or the next child of
 // a leaf list through a per-lane cursor — one step per loop trip.
-template <uint32_t F, int kMode, bool kStats>
+template <uint32_t F, int kMode, bool kStats, class G>
 __device__ __forceinline__ bool trace_stack(const RenderParams& P, const Nodes<kMode>& N, f3 wo, f3 wd, float time,
-                                            Path& path, HitRef& h, uint32_t* stk, Counters& cnt, bool& overflow) {
+                                            G& path, HitRef& h, uint32_t* stk, Counters& cnt, bool& overflow) {
   f3 o = wo, d = wd;
   const f3 winv = recip3(wd);
   f3 inv = winv;
@@ -1103,8 +1131,8 @@ __device__ __forceinline__ uint32_t wave_min_next(uint32_t next) {
   return i;
 }
 
-template <uint32_t F, bool kStats>
-__device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd, float time, Path& path, HitRef& h,
+template <uint32_t F, bool kStats, class G>
+__device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd, float time, G& path, HitRef& h,
                                              Counters& cnt) {
   const Nodes<kModeLinear> N{reinterpret_cast<const float4*>(P.lind)};  // boundaries / nested xforms
 #if !RT2_WIDE_PROGRAM
@@ -1479,17 +1507,17 @@ __device__ __forceinline__ f3 tex_value(const ShadeArgs& S, uint32_t idx, f3 p) 
 }
 
 // ------------------------------------------------------------------------------------------
-template <uint32_t F>
-__device__ __forceinline__ void camera_ray(const RenderParams& P, Path& g, f3& o, f3& d, float& time) {
+template <uint32_t F, class G>
+__device__ __forceinline__ void camera_ray(const RenderParams& P, G& g, f3& o, f3& d, float& time) {
   const CameraParams& C = P.cam;
   const int x = (int)(g.xy & 0xFFFFu), y = (int)(g.xy >> 16);
   const int s_i = (int)(g.sij & 0xFFFFu), s_j = (int)(g.sij >> 16);
   float u[3];
   bool defocus = Has<F, kFeatDefocus>() && !(C.defocus_angle <= 0.0f);
   if (defocus) {
-    g.take<2>(u);
+    g.template take<2>(u);
   } else {
-    g.take<3>(u);  // px, py, time
+    g.template take<3>(u);  // px, py, time
   }
 #if RT2_KARG_CAMERA
   // pixel00, du, dv, center (words 0-11) and recip_sqrt_spp (word 19) from the argument segment
@@ -1516,7 +1544,7 @@ __device__ __forceinline__ void camera_ray(const RenderParams& P, Path& g, f3& o
     if (defocus) {
       // RandInUnitDisk (uniform in the unit disk) by the inverse-CDF map r = sqrt(u), phi = 2 pi v
       float w[2];
-      g.take<2>(w);
+      g.template take<2>(w);
       const float rr = sqrtf(w[0]);
       float cd, sd;
       cos_sin_2pi(w[1], cd, sd);
@@ -1545,9 +1573,10 @@ __device__ __forceinline__ uint32_t local_index(const LoopArgs& A, uint32_t xy) 
 }
 
 // Occupancy target (waves per SIMD the register allocation must allow), chosen per variant by
-// measurement: Cornell 7 (no spills), Cornell volume 6 and the book 2 / all-features stack kernels
-// 6 (some spills, faster than fewer waves: their loads are latency bound), book 1 6. Other stack
-// and the counting kernels keep the compiler's own allocation.
+// measurement (threaded kernels, round 2): Cornell 8 (7: -3 %), Cornell volume 8 (7: -2 %), book 1
+// 8, book 2 7 (6: -3 %; spills VGPRs, but its scalar loads are latency bound), the book 2 /
+// all-features stack kernels 6. Other stack and the counting kernels keep the compiler's own
+// allocation.
 template <uint32_t F, int kMode, bool kStats>
 constexpr int MinWaves() {
   if (RT2_MIN_WAVES_PER_EU > 0) return RT2_MIN_WAVES_PER_EU;
@@ -1556,26 +1585,37 @@ constexpr int MinWaves() {
     return RT2_MIN_WAVES_ALL;  // book 2
   if (F == kBook2 && !kStats && kMode == kModeLinear) return RT2_MIN_WAVES_B2LIN;
   if (kStats || kMode != kModeLinear) return 1;
-  if (F == kFeatXform) return RT2_MIN_WAVES_CORNELL;  // Cornell: 70 VGPRs at 7
-  if (F == (kFeatXform | kFeatMedium)) return RT2_MIN_WAVES_VOL;  // Cornell volume: 89 VGPRs at 5
+  if (F == kFeatXform) return RT2_MIN_WAVES_CORNELL;  // Cornell: 64 VGPRs at 8
+  if (F == (kFeatXform | kFeatMedium)) return RT2_MIN_WAVES_VOL;  // Cornell volume: 64 VGPRs at 8
   if (F == kFeatAll) return 1;
   return RT2_MIN_WAVES_BOOK1;                     // book 1
 }
 
-// Sample octets staged in LDS (rt2_layout.h kOctet): a lane keeps the first 7 samples of an octet in
-// LDS planes and writes the whole octet (96 B, three full 32-B sectors) with six 16-B stores when
-// the 8th is done; a chunk edge inside an octet writes its samples one by one. 5.25 KB per wave:
-// the threaded kernels at <= 7 waves per SIMD (147 KB per CU); other kernels store directly.
+// Samples staged in LDS (rt2_layout.h kOctet): a lane keeps the first samples of a group of
+// consecutive frames in LDS planes and writes the group with 16-B stores when its last sample is
+// done; a chunk edge inside a group writes its samples one by one. Groups of 8 (an octet: 96 B,
+// three whole 32-B sectors; 5.25 KB of LDS per wave, so at most 7 waves per SIMD) or, for kernels
+// at 8 waves, of 4 (48 B; 2.25 KB per wave; the middle sector of an octet is written in two halves,
+// 4/3 of the sample bytes reach memory). Returns the group size, 0 = direct 12-B stores.
+// The threaded product kernels at 8 waves per SIMD keep the Philox block in LDS (PathT; 1 KB per
+// wave): four VGPRs fewer live across the loop, which removed the Cornell kernel's spills at 8
+// waves (12 VGPRs; +1 %, Cornell volume +3 %). Book 2 at 7 waves keeps it in VGPRs (-2 % in LDS).
 template <uint32_t F, int kMode, bool kStats>
-constexpr bool OctetStaged() {
-  return RT2_OCTET_STAGE && kMode == kModeLinear && !kStats && MinWaves<F, kMode, kStats>() <= 7;
+constexpr bool LdsRng() {
+  return RT2_LDS_RNG && kMode == kModeLinear && !kStats && MinWaves<F, kMode, kStats>() >= 8;
 }
-constexpr uint32_t kOctPlanes = 3u * (kOctet - 1u);  // [slot][component] planes of 64 lanes
+template <uint32_t F, int kMode, bool kStats>
+constexpr uint32_t StageGroup() {
+  if (!RT2_OCTET_STAGE || kMode != kModeLinear || kStats) return 0u;
+  // octets need 5.25 KB per wave: with the LDS Philox blocks beside them they fit no occupancy >= 7
+  return MinWaves<F, kMode, kStats>() <= 7 && !LdsRng<F, kMode, kStats>() ? 8u : 4u;
+}
 
 template <uint32_t F, int kMode, bool kStats>
 __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render_kernel(const RenderParams P) {
   constexpr bool kLds = kMode == kModeStackLds || kMode == kModeStackHybrid;
-  constexpr bool kOct = OctetStaged<F, kMode, kStats>();
+  constexpr uint32_t kGroup = StageGroup<F, kMode, kStats>();
+  constexpr uint32_t kPlanes = kGroup ? 3u * (kGroup - 1u) : 1u;  // [slot][component] planes of 64 lanes
   Nodes<kMode> N{reinterpret_cast<const float4*>(P.nodes), P.lds_nodes};
   if constexpr (kLds) {
     const float4* src = reinterpret_cast<const float4*>(P.nodes);
@@ -1585,9 +1625,9 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
   uint32_t* stk = reinterpret_cast<uint32_t*>(s_dyn + (kLds ? P.lds_nodes : 0u)) + threadIdx.x;
   const int lane = (int)__lane_id();
   float* oct_wave = nullptr;  // this wave's staging planes (wave-uniform; lanes add their id)
-  if constexpr (kOct) {
-    __shared__ float s_oct[(kBlock / 64) * kOctPlanes * 64];
-    oct_wave = s_oct + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * (kOctPlanes * 64u);
+  if constexpr (kGroup != 0u) {
+    __shared__ float s_oct[(kBlock / 64) * kPlanes * 64];
+    oct_wave = s_oct + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * (kPlanes * 64u);
   }
   const f3 bg = mk(P.background[0], P.background[1], P.background[2]);
   bool need = true;   // lane wants a work item
@@ -1596,7 +1636,13 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
   unsigned long long rays = 0;  // rays cast by the wave (popcounts of a ballot at the loop head)
   uint32_t bnext = 0, bend = 0;  // the wave's reserved batch of work items (wave-uniform)
   uint32_t item_rays = 0;
-  Path path;
+  constexpr bool kLdsRng = LdsRng<F, kMode, kStats>();
+  PathT<kLdsRng> path;
+  path.rbw = nullptr;
+  if constexpr (kLdsRng) {
+    __shared__ uint32_t s_rng[(kBlock / 64) * 4 * 64];
+    path.rbw = s_rng + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * 256u;
+  }
   path.k0 = P.seed_lo;
   path.k1 = P.seed_hi;
   path.width = (uint32_t)P.width;
@@ -1605,8 +1651,8 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
   path.r0 = path.r1 = path.r2 = path.r3 = 0;
   f3 ro = mk(0, 0, 0), rd = mk(0, 0, 1), thr = mk(1, 1, 1);
   float rtime = 0.0f;
-  // depth_left (RayColor's depth, bits 0-15) | frames of the lane's chunk after this one (bits 16-28)
-  // | the first octet slot this lane holds in the current octet (bits 29-31)
+  // depth_left (RayColor's depth, bits 0-15) | frames of the lane's chunk after this one (bits 16-26)
+  // | the lane's first octet slot in the current octet (bits 27-31, sample staging)
   uint32_t dl = 0;
   Counters cnt = {};
   bool overflow = false;
@@ -1694,7 +1740,8 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
             path.sij = ce[1];  // then advanced per frame below
             camera_ray<F>(P, path, ro, rd, rtime);
             thr = mk(1, 1, 1);
-            dl = max_depth | ((uint32_t)(fstop - f - 1) << 16) | (((uint32_t)(f - A.frame_begin()) & (kOctet - 1u)) << 29);
+            const uint32_t s0 = (uint32_t)(f - A.frame_begin()) & (kOctet - 1u);
+            dl = max_depth | ((uint32_t)(fstop - f - 1) << 16) | (s0 << 27);
           }
         }
       }
@@ -1723,7 +1770,7 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
           f3 ro2 = ro;
           asm volatile("" : "+v"(ro2.x), "+v"(ro2.y), "+v"(ro2.z));
           HitRef h2;
-          Path p2 = path;
+          auto p2 = path;
           bool hit2 = trace_linear<F, kStats>(P, ro2, rd, rtime, p2, h2, cnt);
           asm volatile("" ::"v"(h2.t), "v"(h2.prim), "v"(h2.xf), "v"((int)hit2));
         }
@@ -1770,7 +1817,7 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
           if (!dielectric) ru = rand_unit_vec3(path);  // one sampling site for every other material
 #if RT2_EXP_TWICE & 2
           {
-            Path p2 = path;
+            auto p2 = path;
             asm volatile("" : "+v"(p2.n), "+v"(p2.frame));
             f3 r2 = rand_unit_vec3(p2);
             asm volatile("" ::"v"(r2.x), "v"(r2.y), "v"(r2.z));
@@ -1820,31 +1867,33 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
       const uint32_t slot = fr & (kOctet - 1u);
       float* blk = A.samples() + 3ull * kOctet * ((unsigned long long)(fr / kOctet) * A.local_pixels() + lidx);
       const bool more = ((dl >> 16) & kChunkLeftMask) != 0u;  // frames of the chunk after this one
-      if constexpr (kOct) {
+      if constexpr (kGroup != 0u) {
         float* oct = oct_wave + __lane_id();
-        if (slot == kOctet - 1u || !more) {
-          const uint32_t first = dl >> 29;
-          if (first == 0u && slot == kOctet - 1u) {  // the whole octet: six 16-B stores
-            float4* b4 = reinterpret_cast<float4*>(blk);
+        const uint32_t gs = slot & (kGroup - 1u);  // slot within the group = LDS slot
+        if (gs == kGroup - 1u || !more) {
+          const uint32_t g0 = slot - gs;  // the group's first octet slot
+          const uint32_t first = max(dl >> 27, g0) - g0;  // this lane's first LDS slot of the group
+          if (first == 0u && gs == kGroup - 1u) {  // the whole group: 16-B stores
+            float4* b4 = reinterpret_cast<float4*>(blk + 3u * g0);
 #pragma unroll
-            for (uint32_t j = 0; j < 5; j++)  // planes 4j..4j+3 (one 16-B store each, few live registers)
+            for (uint32_t j = 0; j + 1u < 3u * kGroup / 4u; j++)  // planes 4j..4j+3, few live registers
               b4[j] = make_float4(oct[64u * (4u * j)], oct[64u * (4u * j + 1u)], oct[64u * (4u * j + 2u)],
                                   oct[64u * (4u * j + 3u)]);
-            b4[5] = make_float4(oct[64u * 20u], color.x, color.y, color.z);
-          } else {  // a chunk edge inside the octet: this lane's slots first..slot
-            for (uint32_t k = first; k < slot; k++) {
-              blk[3u * k] = oct[64u * (3u * k)];
-              blk[3u * k + 1u] = oct[64u * (3u * k + 1u)];
-              blk[3u * k + 2u] = oct[64u * (3u * k + 2u)];
+            b4[3u * kGroup / 4u - 1u] = make_float4(oct[64u * (kPlanes - 1u)], color.x, color.y, color.z);
+          } else {  // a chunk edge inside the group: this lane's slots first..gs
+            for (uint32_t k = first; k < gs; k++) {
+              blk[3u * (g0 + k)] = oct[64u * (3u * k)];
+              blk[3u * (g0 + k) + 1u] = oct[64u * (3u * k + 1u)];
+              blk[3u * (g0 + k) + 2u] = oct[64u * (3u * k + 2u)];
             }
             blk[3u * slot] = color.x;
             blk[3u * slot + 1u] = color.y;
             blk[3u * slot + 2u] = color.z;
           }
         } else {
-          oct[64u * (3u * slot)] = color.x;
-          oct[64u * (3u * slot + 1u)] = color.y;
-          oct[64u * (3u * slot + 2u)] = color.z;
+          oct[64u * (3u * gs)] = color.x;
+          oct[64u * (3u * gs + 1u)] = color.y;
+          oct[64u * (3u * gs + 2u)] = color.z;
         }
       } else {
         blk[3u * slot] = color.x;
@@ -1865,7 +1914,7 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
         }
 #if RT2_EXP_TWICE & 4
         {
-          Path p2 = path;
+          auto p2 = path;
           f3 o2, d2;
           float t2;
           asm volatile("" : "+v"(p2.frame), "+v"(p2.sij));
@@ -1876,7 +1925,7 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
         camera_ray<F>(P, path, ro, rd, rtime);
         thr = mk(1, 1, 1);
         // one frame fewer left; after the octet's last slot the next octet starts at slot 0
-        dl = (((dl & 0x1FFF0000u) - 0x10000u) | (uint32_t)A.max_depth()) | (slot == kOctet - 1u ? 0u : (dl & 0xE0000000u));
+        dl = (((dl & 0x07FF0000u) - 0x10000u) | (uint32_t)A.max_depth()) | (slot == kOctet - 1u ? 0u : (dl & 0xF8000000u));
       } else {
         if (kStats && P.ray_counts) atomicAdd(P.ray_counts + lidx, item_rays);
         need = true;

@@ -169,9 +169,9 @@ struct Magic {
 // A lane writes a whole octet at once (three full 32-B sectors) instead of 12 B at a time.
 constexpr uint32_t kOctet = 8;
 // Frame chunks hold at most kChunkMaxFrames frames: the kernel keeps a chunk's frames left in
-// 13 bits of a register that also holds the ray depth and the lane's first octet slot.
-constexpr int kChunkMaxFrames = 0x2000;
-constexpr uint32_t kChunkLeftMask = 0x1FFFu;
+// 11 bits of a register that also holds the ray depth and the lane's sample-staging state.
+constexpr int kChunkMaxFrames = 0x800;
+constexpr uint32_t kChunkLeftMask = 0x7FFu;
 
 struct RenderParams {
   const void* nodes;      // float4[]
