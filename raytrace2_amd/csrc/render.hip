@@ -112,6 +112,9 @@ constexpr int kBlock = 256;
 #ifndef RT2_LDS_RNG
 #define RT2_LDS_RNG 1  // threaded kernels: the lane's Philox block in LDS rather than live VGPRs
 #endif
+#ifndef RT2_RAW_MINMAX
+#define RT2_RAW_MINMAX 1  // slab tests: single v_min/v_max instructions (no operand quieting)
+#endif
 #ifndef RT2_OCTET_STAGE
 #define RT2_OCTET_STAGE 1  // threaded kernels at <= 7 waves: stage a lane's samples in LDS, one 96-B store per octet
 #endif
@@ -602,13 +605,55 @@ __device__ __forceinline__ bool aabb_hit(float4 lo, float4 hi, f3 o, f3 inv, flo
 
 // aabb_hit when no slab value can be NaN (inv finite, so (bound - o) * inv is finite or +-inf):
 // the swap + glm::max/min chain with early exits then equals min/max of all axes at once.
+// min / max of the slab tests as single instructions. fminf / fmaxf (IEEE minNum / maxNum) make the
+// compiler quiet possible signalling NaNs first (a v_max_f32 x, x per operand it cannot prove
+// canonical: loop-carried tmax, values from another block); every operand here comes out of a
+// VALU operation or is a finite record bound, so it is never a signalling NaN, and v_min_f32 /
+// v_max_f32 already return the other operand for a quiet NaN: the same values, minNum / maxNum
+// semantics included (the padded slab test relies on NaN being ignored).
+#if RT2_RAW_MINMAX
+__device__ __forceinline__ float vmin(float a, float b) {
+  float r;
+  asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ float vmax(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ float vmin3(float a, float b, float c) {
+  float r;
+  asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ float vmax3(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+#else
+__device__ __forceinline__ float vmin(float a, float b) { return fminf(a, b); }
+__device__ __forceinline__ float vmax(float a, float b) { return fmaxf(a, b); }
+__device__ __forceinline__ float vmin3(float a, float b, float c) { return fminf(fminf(a, b), c); }
+__device__ __forceinline__ float vmax3(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
+#endif
+// t0 = max(min(ax, bx), min(ay, by), min(az, bz), tmin), t1 likewise: max and min are associative
+// and commutative on these operands (NaN aside, which the callers exclude or which minNum ignores
+// in any grouping), so the grouping below gives the reference's values.
+__device__ __forceinline__ void slab_t(float ax, float bx, float ay, float by, float az, float bz, float tmin,
+                                       float tmax, float& t0, float& t1) {
+  t0 = vmax3(vmin(ax, bx), vmin(ay, by), vmax(vmin(az, bz), tmin));
+  t1 = vmin3(vmax(ax, bx), vmax(ay, by), vmin(vmax(az, bz), tmax));
+}
+
 __device__ __forceinline__ bool aabb_hit_fin(float4 lo, float4 hi, f3 o, f3 inv, float tmin, float tmax) {
   const float ax = (lo.x - o.x) * inv.x, bx = (hi.x - o.x) * inv.x;
   const float ay = (lo.y - o.y) * inv.y, by = (hi.y - o.y) * inv.y;
   const float az = (lo.z - o.z) * inv.z, bz = (hi.z - o.z) * inv.z;
-  const float t0 = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), tmin));
-  const float t1 = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), tmax));
-  return !(t1 <= t0);
+  float t0, t1;
+  slab_t(ax, bx, ay, by, az, bz, tmin, tmax, t0, t1);
+  return !(t1 <= t0);  // AABB::Hit: a miss when t1 <= t0 (AABB.hpp)
 }
 __device__ __forceinline__ bool finite3(f3 v) {
   return __builtin_isfinite(v.x) && __builtin_isfinite(v.y) && __builtin_isfinite(v.z);
@@ -1346,8 +1391,8 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
       const float ax = ((uf(aw[4]) - acc_pad) - o.x) * inv.x, bx = ((uf(aw[8]) + acc_pad) - o.x) * inv.x;
       const float ay = ((uf(aw[5]) - acc_pad) - o.y) * inv.y, by = ((uf(aw[9]) + acc_pad) - o.y) * inv.y;
       const float az = ((uf(aw[6]) - acc_pad) - o.z) * inv.z, bz = ((uf(aw[10]) + acc_pad) - o.z) * inv.z;
-      const float t0 = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), tmin));
-      const float t1 = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), tmax));
+      float t0, t1;
+      slab_t(ax, bx, ay, by, az, bz, tmin, tmax, t0, t1);
       if (!(t0 <= t1)) next = st.y;
     } else if (Has<F, kFeatAccList>() && kind == kAccSphere) {
       RT2_STEP_WORDS(aw);
