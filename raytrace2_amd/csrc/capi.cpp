@@ -91,7 +91,7 @@ struct rt2_tracer {
   size_t sample_budget = size_t(16) << 30;  // bytes; bounds the frames per launch
   int work_split = 16;                     // chunk schedule: work left split into >= k items per lane (0: one chunk)
   int chunk_max = 64;                      // longest chunk (frames)
-  bool chunk_align = true;                 // chunks of >= kOctet frames fill whole sample octets
+  bool chunk_align = true;                 // chunks of >= kOctet frames: multiples of 4 frames
   uint32_t* d_chunks = nullptr;            // chunk table of the last launch shape (ChunkSchedule)
   size_t chunks_bytes = 0;
   uint32_t n_chunks = 0;
@@ -776,7 +776,9 @@ int ChunkSchedule(rt2_tracer* t, int fb, int n, uint32_t tile_items, int64_t lan
       const double want = (double)(n - s) * (double)tile_items / ((double)t->work_split * (double)lanes);
       len = (int)std::min<double>(want, (double)t->chunk_max);
     }
-    if (t->chunk_align && len >= (int)kOctet) len -= len % (int)kOctet;  // long chunks fill whole sample octets
+    // long chunks start on a 4-frame group of the sample octets (the 8-wave kernels stage samples
+    // by 4 frames; whole octets would cut a 15-frame chunk to 8)
+    if (t->chunk_align && len >= (int)kOctet) len -= len % 4;
     len = std::max(len, lo);
     len = std::min({len, n - s, kChunkMaxFrames});
     const uint32_t f = (uint32_t)(fb + s), usq = (uint32_t)sq;
