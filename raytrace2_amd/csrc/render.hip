@@ -289,6 +289,24 @@ __device__ __forceinline__ u32x8 karg8() {
                : "s"(__builtin_amdgcn_kernarg_segment_ptr()), "n"(kOff));
   return v;
 }
+template <uint32_t kOff>
+__device__ __forceinline__ u32x4 karg4() {
+  static_assert(kOff % 4 == 0, "dword-aligned");
+  u32x4 v;
+  asm volatile("s_load_dwordx4 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)"
+               : "=s"(v)
+               : "s"(__builtin_amdgcn_kernarg_segment_ptr()), "n"(kOff));
+  return v;
+}
+template <uint32_t kOff>
+__device__ __forceinline__ unsigned long long karg2() {
+  static_assert(kOff % 4 == 0, "dword-aligned");
+  unsigned long long v;
+  asm volatile("s_load_dwordx2 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)"
+               : "=s"(v)
+               : "s"(__builtin_amdgcn_kernarg_segment_ptr()), "n"(kOff));
+  return v;
+}
 
 #define RT2_KOFF(f) ((uint32_t)offsetof(RenderParams, f))
 template <typename T, int k>
@@ -337,6 +355,7 @@ struct LoopArgs {
   RT2_LA(batch_max, uint32_t, batch_max)
   RT2_LA(batch_div, uint32_t, batch_div)
   RT2_LA(frame_begin, int, frame_begin)
+  RT2_LA(n_frames, int, n_frames)
   RT2_LA(max_depth, int, max_depth)
   RT2_LA(chunks, const uint32_t*, chunks)
   RT2_LA(div_tile_items, Magic, div_tile_items)
@@ -1755,20 +1774,36 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
         if (item >= A.n_items()) {
           idle = true;  // no work left for this lane
         } else {
-          const uint32_t chunk = udiv(item, A.div_tile_items());  // chunk-major: every tile's chunk 0 first
-          const uint32_t titem = item - chunk * A.tile_items();
-          const uint32_t tile = titem >> 6, within = titem & 63u;
-          const uint32_t trow = udiv(tile, A.div_tiles_x());
-          // tiles of (64 >> tile_shift) local rows x (1 << tile_shift) pixels
-          const uint32_t tsh = A.tile_shift(), tw = 1u << tsh;
-          const int x = (int)((tile - trow * (uint32_t)A.tiles_x()) * tw + (within & (tw - 1u)));
-          const int r = (int)(trow * (64u >> tsh) + (within >> tsh));
+          uint32_t chunk;
+          int x, r;
+          static_assert(RT2_KOFF(frame_tile) == RT2_KOFF(frame_tiles) + 4 &&
+                            RT2_KOFF(div_frame_tile) == RT2_KOFF(frame_tiles) + 8, "RenderParams layout");
+          const u32x4 ft = karg4<RT2_KOFF(frame_tiles)>();  // frame_tiles, frame_tile, div_frame_tile
+          if (ft[0] != 0u) {  // frame tiles: one pixel x 64 consecutive one-frame chunks per 64 items
+            const unsigned long long dw = karg2<RT2_KOFF(div_width)>();
+            const uint32_t g = udiv(item, Magic{ft[2], ft[3]});
+            const uint32_t rem = item - g * ft[1];
+            const uint32_t pix = rem >> 6;
+            chunk = g * 64u + (rem & 63u);
+            r = (int)udiv(pix, Magic{(uint32_t)dw, (uint32_t)(dw >> 32)});
+            x = (int)(pix - (uint32_t)r * (uint32_t)A.width());
+          } else {
+            chunk = udiv(item, A.div_tile_items());  // chunk-major: every tile's chunk 0 first
+            const uint32_t titem = item - chunk * A.tile_items();
+            const uint32_t tile = titem >> 6, within = titem & 63u;
+            const uint32_t trow = udiv(tile, A.div_tiles_x());
+            // tiles of (64 >> tile_shift) local rows x (1 << tile_shift) pixels
+            const uint32_t tsh = A.tile_shift(), tw = 1u << tsh;
+            x = (int)((tile - trow * (uint32_t)A.tiles_x()) * tw + (within & (tw - 1u)));
+            r = (int)(trow * (64u >> tsh) + (within >> tsh));
+          }
           // the chunk's first frame and its stratum (RayTracer.cpp:59-60, from the host's table),
           // and the next chunk's first frame (<= first + kChunkMaxFrames)
           const uint32_t* ce = A.chunks() + 2u * chunk;
           const int f = (int)ce[0];
           const int fstop = (int)ce[2];
-          if (x < A.width() && r < A.local_rows()) {  // else: a lane of a partial edge tile
+          // else: a lane of a partial edge tile, or a padding chunk of the frame tiles
+          if (x < A.width() && r < A.local_rows() && f < A.frame_begin() + A.n_frames()) {
             uint32_t y = (uint32_t)r;
             const uint32_t world = (uint32_t)A.world();
             if (world > 1u) {  // local row -> global row (rt2_layout.h BandRank)

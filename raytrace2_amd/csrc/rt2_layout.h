@@ -213,6 +213,12 @@ struct RenderParams {
   const void* lind;        // float4 records of the program's steps (kModeLinear)
   const void* lin_wide;    // 64-byte steps: entry + first 48 bytes of its record (kModeLinear)
   uint32_t lin_len;
+  // Frame tiles (item mode 1): a wave's 64 items are one pixel x 64 consecutive frames of the launch
+  // (chunks of one frame), so its lanes trace paths from the same pixel. item = g * frame_tile +
+  // pixel * 64 + k renders chunk 64 g + k of local pixel `pixel`; frame_tile = 64 * local_pixels.
+  uint32_t frame_tiles;
+  uint32_t frame_tile;
+  Magic div_frame_tile, div_width;
 };
 
 }  // namespace rt2
