@@ -104,3 +104,21 @@ def test_spp20_sq2_below_spp_frames_wrap(split):
 def test_frames_beyond_sq2_in_several_launches():
     """spp 16 (sq 4), 40 frames as launches of 7 frames: launch boundaries inside the cycle."""
     _check("cornell_box_volume", 64, 48, 16, 40, launch_frames=7)
+
+
+@pytest.mark.parametrize("name,w,h,spp,frames,part", [
+    ("cornell_box_original", 72, 40, 20, 40, {}),                                  # frames past sq^2, 64-frame groups padded
+    ("cornell_box_volume", 1024, 1024, 4000, 70, dict(band_h=8, rank=40, world=128)),  # a band, one padded group
+    ("final_render_book_1", 64, 48, 16, 130, {}),                                  # defocus, 3 groups
+])
+def test_frame_tiles_forced(monkeypatch, name, w, h, spp, frames, part):
+    """Frame tiles (a wave = one pixel x 64 one-frame chunks; book 2 runs them by default) forced on
+    scenes that default to pixel tiles: the same bits as the oracle."""
+    monkeypatch.setenv("RT2_FRAME_TILES", "1")
+    _check(name, w, h, spp, frames, **part)
+
+
+def test_frame_tiles_off_on_book2(monkeypatch):
+    """Book 2 with frame tiles switched off (pixel tiles, 64-frame chunks) against the oracle."""
+    monkeypatch.setenv("RT2_FRAME_TILES", "0")
+    _check("book2_final_scene_10000_samples", 800, 800, 10000, 12, band_h=8, rank=50, world=100)

@@ -189,3 +189,14 @@ def test_camera_setter_on_multi_tracer():
         assert tr.get_camera() == cam_b
         tr.close()
     assert _same(outs[0], outs[1])
+
+
+def test_partitions_with_frame_tiles(monkeypatch):
+    """Frame tiles (one pixel x 64 frames per wave) on a 3-way loopback partition: the gathered image
+    equals one plain render."""
+    monkeypatch.setenv("RT2_FRAME_TILES", "1")
+    w, h, spp, frames = 50, 45, 16, 70
+    acc, px, rc, st = _plain("cornell_box_original", w, h, spp, frames)
+    macc, mpx, mrc, mst, _ = _multi("cornell_box_original", w, h, spp, frames, devices=[0] * 3, band_h=2)
+    assert _same(macc, acc) and np.array_equal(mpx, px) and np.array_equal(mrc, rc)
+    assert mst["rays"] == st["rays"]
