@@ -92,7 +92,7 @@ constexpr int kBlock = 256;
 #define RT2_MIN_WAVES_BOOK1 8
 #endif
 #ifndef RT2_MIN_WAVES_VOL
-#define RT2_MIN_WAVES_VOL 8
+#define RT2_MIN_WAVES_VOL 7
 #endif
 #ifndef RT2_MIN_WAVES_B2LIN
 #define RT2_MIN_WAVES_B2LIN 7  // book 2 threaded: 3/4/5/6/7/8 waves 934/938/1091/1183/1297/508 Mray/s
@@ -1637,8 +1637,9 @@ __device__ __forceinline__ uint32_t local_index(const LoopArgs& A, uint32_t xy) 
 }
 
 // Occupancy target (waves per SIMD the register allocation must allow), chosen per variant by
-// measurement (threaded kernels, round 2): Cornell 8 (7: -3 %), Cornell volume 8 (7: -2 %), book 1
-// 8, book 2 7 (6: -3 %; spills VGPRs, but its scalar loads are latency bound), the book 2 /
+// measurement (threaded kernels, round 2): Cornell 8 (7: -3 %), Cornell volume 7 (8 with the Philox
+// block in LDS: the same speed, more spill traffic), book 1 8, book 2 7 (6: -3 %; spills VGPRs, but
+// its scalar loads are latency bound), the book 2 /
 // all-features stack kernels 6. Other stack and the counting kernels keep the compiler's own
 // allocation.
 template <uint32_t F, int kMode, bool kStats>
@@ -1650,7 +1651,7 @@ constexpr int MinWaves() {
   if (F == kBook2 && !kStats && kMode == kModeLinear) return RT2_MIN_WAVES_B2LIN;
   if (kStats || kMode != kModeLinear) return 1;
   if (F == kFeatXform) return RT2_MIN_WAVES_CORNELL;  // Cornell: 64 VGPRs at 8
-  if (F == (kFeatXform | kFeatMedium)) return RT2_MIN_WAVES_VOL;  // Cornell volume: 64 VGPRs at 8
+  if (F == (kFeatXform | kFeatMedium)) return RT2_MIN_WAVES_VOL;  // Cornell volume: 72 VGPRs at 7
   if (F == kFeatAll) return 1;
   return RT2_MIN_WAVES_BOOK1;                     // book 1
 }
@@ -1663,7 +1664,8 @@ constexpr int MinWaves() {
 // 4/3 of the sample bytes reach memory). Returns the group size, 0 = direct 12-B stores.
 // The threaded product kernels at 8 waves per SIMD keep the Philox block in LDS (PathT; 1 KB per
 // wave): four VGPRs fewer live across the loop, which removed the Cornell kernel's spills at 8
-// waves (12 VGPRs; +1 %, Cornell volume +3 %). Book 2 at 7 waves keeps it in VGPRs (-2 % in LDS).
+// waves (12 VGPRs; +1 %). The 7-wave kernels (book 2, Cornell volume) keep it in VGPRs (book 2: -2 % in
+// LDS) and stage whole sample octets instead.
 template <uint32_t F, int kMode, bool kStats>
 constexpr bool LdsRng() {
   return RT2_LDS_RNG && kMode == kModeLinear && !kStats && MinWaves<F, kMode, kStats>() >= 8;
