@@ -92,7 +92,8 @@ struct rt2_tracer {
   int work_split = 16;                     // chunk schedule: work left split into >= k items per lane (0: one chunk)
   int chunk_max = 64;                      // longest chunk (frames)
   int frame_tiles_env = -1;                // RT2_FRAME_TILES: -1 auto, 0 off, 1 on
-  bool frame_tiles = false;                // this launch: items = one pixel x 64 one-frame chunks per wave
+  bool frame_tiles = false;                // this launch: items = one pixel x 64 short chunks per wave
+  int frame_tile_len = 8;                  // most frames per chunk in frame-tile mode (RT2_FRAME_TILE_LEN)
   bool chunk_align = true;                 // chunks of >= kOctet frames: multiples of 4 frames
   uint32_t* d_chunks = nullptr;            // chunk table of the last launch shape (ChunkSchedule)
   size_t chunks_bytes = 0;
@@ -520,6 +521,7 @@ int rt2_tracer_create(const rt2_scene* s, int device, rt2_tracer** out) {
   if (const char* e = getenv("RT2_CHUNK_MAX")) t->chunk_max = std::max(1, atoi(e));
   if (const char* e = getenv("RT2_CHUNK_ALIGN")) t->chunk_align = e[0] != '0';
   if (const char* e = getenv("RT2_FRAME_TILES")) t->frame_tiles_env = e[0] == '1' ? 1 : 0;
+  if (const char* e = getenv("RT2_FRAME_TILE_LEN")) t->frame_tile_len = std::max(1, std::min(atoi(e), 64));
   // App.cpp:122-125,157: scene dims when present, else the window default 1600x900
   int w = s->scene.dims_x > 0 && s->scene.dims_y > 0 ? s->scene.dims_x : 1600;
   int h = s->scene.dims_x > 0 && s->scene.dims_y > 0 ? s->scene.dims_y : 900;
@@ -750,7 +752,7 @@ int rt2_tracer_get_camera(const rt2_tracer* t, rt2_camera_desc* o) {
 }  // extern "C"
 
 namespace {
-constexpr uint32_t kFrameTileMinSteps = 2048;  // threaded programs longer than this use frame tiles
+constexpr uint32_t kFrameTileMinSteps = 256;  // threaded programs longer than this use frame tiles
 
 Magic MakeMagic(uint32_t d) {  // rt2_layout.h Magic: floor(n / d) for n < 2^31
   uint32_t l = 0;
@@ -769,17 +771,24 @@ int ChunkSchedule(rt2_tracer* t, int fb, int n, uint32_t tile_items, int64_t lan
   const uint64_t key[6] = {(uint64_t)fb, (uint64_t)n, tile_items, (uint64_t)lanes,
                            (uint64_t)t->work_split | ((uint64_t)t->chunk_max << 32) | ((uint64_t)t->chunk_align << 63) |
                                ((uint64_t)t->frame_tiles << 62),
-                           (uint64_t)sq};
+                           (uint64_t)sq | ((uint64_t)t->frame_tile_len << 32)};
   if (t->d_chunks && memcmp(key, t->chunk_key, sizeof(key)) == 0) return RT2_OK;
   // items must stay below 2^31 (kernel index arithmetic): shortest chunk that allows it
   const int64_t max_chunks = std::max<int64_t>(1, (int64_t)0x7FFFFFFF / tile_items);
   const int lo = (int)std::max<int64_t>(1, ((int64_t)n + max_chunks - 1) / max_chunks);
   std::vector<uint32_t> tab;
   int first = 0;
+  // frame tiles: chunks of up to frame_tile_len frames, as even as the 64-chunk groups allow (the
+  // last group is padded with empty chunks, whose lanes fetch again)
+  int ft_len = 1;
+  if (t->frame_tiles) {
+    const int groups = (n + 64 * t->frame_tile_len - 1) / (64 * t->frame_tile_len);
+    ft_len = (n + 64 * groups - 1) / (64 * groups);
+  }
   for (int s = 0; s < n;) {
     int len = n - s;
     if (t->frame_tiles) {
-      len = 1;  // frame tiles: one-frame chunks (RenderParams::frame_tiles)
+      len = ft_len;  // frame tiles: short chunks of one pixel (RenderParams::frame_tiles)
     } else if (t->work_split > 0) {
       const double want = (double)(n - s) * (double)tile_items / ((double)t->work_split * (double)lanes);
       len = (int)std::min<double>(want, (double)t->chunk_max);
@@ -870,9 +879,9 @@ int LaunchFrames(rt2_tracer* t, int n_frames) {
   p.lin_len = t->use_linear ? t->lin_len : 0u;
   // Frame tiles (a wave's lanes trace one pixel's consecutive frames: paths from one pixel share
   // their first hit and start their secondary rays from nearly one point, so the lockstep walk of
-  // a deep program serves more lanes per step) for deep threaded programs: measured book 2
-  // (4,922 steps) +9 %; book 1 (995 steps) -4 %, Cornell -4.5 % (there 8x8 pixel tiles are as
-  // coherent and the per-path item fetch costs more than it saves).
+  // a deep program serves more lanes per step) for deep threaded programs: measured with chunks of
+  // up to 8 frames, book 2 (4,922 steps) +4 %, book 1 (995 steps) +4.5 %; Cornell (29 steps) -2 %,
+  // where 8x8 pixel tiles are as coherent and the shorter chunks cost more item fetches.
   t->frame_tiles = t->frame_tiles_env >= 0 ? t->frame_tiles_env == 1 : (p.lin_len > kFrameTileMinSteps);
   uint32_t feats = t->features | (p.cam.defocus_angle > 0.0f ? (uint32_t)kFeatDefocus : 0u);
   int variant = RenderVariant(feats);

@@ -115,6 +115,9 @@ constexpr int kBlock = 256;
 #ifndef RT2_RAW_MINMAX
 #define RT2_RAW_MINMAX 1  // slab tests: single v_min/v_max instructions (no operand quieting)
 #endif
+#ifndef RT2_BVH_SELECT
+#define RT2_BVH_SELECT 0  // threaded BVH step: branch-free next-index select (experiment)
+#endif
 #ifndef RT2_OCTET_STAGE
 #define RT2_OCTET_STAGE 1  // threaded kernels at <= 7 waves: stage a lane's samples in LDS, one 96-B store per octet
 #endif
@@ -1243,6 +1246,15 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
       do {
         RT2_WAVE(1);
         RT2_WAVE(2);
+#if RT2_BVH_SELECT
+        if (allfin) {  // every lane evaluates the slab test; the lanes at step i take its result
+          if (kStats && next == i) cnt.bvh++;
+          const float4 lo = make_float4(uf(sw[4]), uf(sw[5]), uf(sw[6]), 0.0f);
+          const float4 hi = make_float4(uf(sw[8]), uf(sw[9]), uf(sw[10]), 0.0f);
+          const bool in = aabb_hit_fin(lo, hi, o, inv, tmin, tmax);
+          next = next == i ? (in ? i + 1u : sw[1]) : next;
+        } else
+#endif
         if (next == i) {
           if (kStats) cnt.bvh++;
           const float4 lo = make_float4(uf(sw[4]), uf(sw[5]), uf(sw[6]), 0.0f);
