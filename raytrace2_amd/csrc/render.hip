@@ -118,6 +118,9 @@ constexpr int kBlock = 256;
 #ifndef RT2_BVH_SELECT
 #define RT2_BVH_SELECT 0  // threaded BVH step: branch-free next-index select (experiment)
 #endif
+#ifndef RT2_BVH_SPEC
+#define RT2_BVH_SPEC 0  // threaded BVH run: load step i + 1 while step i's slab test and wave minimum run
+#endif
 #ifndef RT2_OCTET_STAGE
 #define RT2_OCTET_STAGE 1  // threaded kernels at <= 7 waves: stage a lane's samples in LDS, one 96-B store per octet
 #endif
@@ -1246,13 +1249,25 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
       do {
         RT2_WAVE(1);
         RT2_WAVE(2);
-#if RT2_BVH_SELECT
+#if RT2_WIDE_PROGRAM && RT2_BVH_SPEC
+        // i + 1 is the wave's next step whenever a lane at i hits the box (pre-order: the near
+        // child follows), so its 64 bytes are fetched now; the load stays in flight (nothing reads
+        // `spec`) until the wait below, which every path out of this iteration passes
+        const uint32_t pi = i + 1u < len ? i + 1u : i;
+        u32x16 spec;
+        asm volatile("s_load_dwordx16 %0, %1, %2" : "=s"(spec) : "s"(P.lin_wide), "s"(pi * 64u));
+#endif
+#if RT2_BVH_SELECT && RT2_WIDE_PROGRAM
         if (allfin) {  // every lane evaluates the slab test; the lanes at step i take its result
           if (kStats && next == i) cnt.bvh++;
           const float4 lo = make_float4(uf(sw[4]), uf(sw[5]), uf(sw[6]), 0.0f);
           const float4 hi = make_float4(uf(sw[8]), uf(sw[9]), uf(sw[10]), 0.0f);
           const bool in = aabb_hit_fin(lo, hi, o, inv, tmin, tmax);
-          next = next == i ? (in ? i + 1u : sw[1]) : next;
+          bool in2 = true;
+          if (sw[2] != i + 1u)
+            in2 = aabb_hit_fin(make_float4(uf(sw[7]), uf(sw[11]), uf(sw[12]), 0.0f),
+                               make_float4(uf(sw[13]), uf(sw[14]), uf(sw[15]), 0.0f), o, inv, tmin, tmax);
+          next = next == i ? (in ? (in2 ? sw[2] : sw[3]) : sw[1]) : next;
         } else
 #endif
         if (next == i) {
@@ -1260,6 +1275,20 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
           const float4 lo = make_float4(uf(sw[4]), uf(sw[5]), uf(sw[6]), 0.0f);
           const float4 hi = make_float4(uf(sw[8]), uf(sw[9]), uf(sw[10]), 0.0f);
           const bool in = allfin ? aabb_hit_fin(lo, hi, o, inv, tmin, tmax) : aabb_hit(lo, hi, o, inv, tmin, tmax);
+#if RT2_WIDE_PROGRAM
+          // a paired step (compile.cpp: word 2 is not i + 1; sphere scenes only) also tests its near
+          // child's box, with the tmax that child's own step would see (nothing runs between the
+          // two in pre-order)
+          uint32_t nx = in ? i + 1u : sw[1];
+          if (Has<F, kFeatSphere>() && sw[2] != i + 1u) {
+            const float4 lo2 = make_float4(uf(sw[7]), uf(sw[11]), uf(sw[12]), 0.0f);
+            const float4 hi2 = make_float4(uf(sw[13]), uf(sw[14]), uf(sw[15]), 0.0f);
+            const bool in2 =
+                allfin ? aabb_hit_fin(lo2, hi2, o, inv, tmin, tmax) : aabb_hit(lo2, hi2, o, inv, tmin, tmax);
+            if (kStats && in) cnt.bvh++;
+            nx = in ? (in2 ? sw[2] : sw[3]) : sw[1];
+          }
+#endif
 #if RT2_EXP_TWICE & 8
           {
             f3 o2 = o;
@@ -1268,13 +1297,25 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
             asm volatile("" ::"v"((int)in2));
           }
 #endif
+#if RT2_WIDE_PROGRAM
+          next = nx;
+#else
           next = in ? i + 1u : sw[1];
+#endif
         }
         i = wave_min_next(next);
+#if RT2_WIDE_PROGRAM && RT2_BVH_SPEC
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(spec));
         if (i >= len) break;
-#if RT2_WIDE_PROGRAM
+        if (i == pi)
+          sw = spec;
+        else
+          sw = sld16(P.lin_wide, i * 64u);
+#elif RT2_WIDE_PROGRAM
+        if (i >= len) break;
         sw = sld16(P.lin_wide, i * 64u);
 #else
+        if (i >= len) break;
         const u32x4 e = sld4(prog, i * 16u);
         sw[0] = e.x, sw[1] = e.y, sw[2] = e.z, sw[3] = e.w;
         if (e.x == kBvh) {
