@@ -189,6 +189,21 @@ def test_book2_threaded_equals_stack(have_gpu, monkeypatch):
     assert np.array_equal(a1.view(np.uint32), a2.view(np.uint32))
 
 
+@pytest.mark.parametrize("name,w,h,spp,frames", [("final_render_book_1", 96, 54, 500, 4),
+                                                 ("book2_final_scene_10000_samples", 120, 120, 10000, 3)])
+def test_paired_bvh_steps_are_invisible(have_gpu, monkeypatch, name, w, h, spp, frames):
+    """Paired BVH steps (compile.cpp: a step also tests its near child's box, with the tmax the
+    child's own step would see) give bit-identical renders and ray counts to single-box steps, and
+    every lane tests exactly the same boxes (equal box-test counts)."""
+    a1, r1, s1, _ = gpu_render(name, w, h, spp, frames, stats=True)
+    monkeypatch.setenv("RT2_BVH_PAIRS", "0")
+    a2, r2, s2, _ = gpu_render(name, w, h, spp, frames, stats=True)
+    assert s1["overflow"] == 0 and s2["overflow"] == 0
+    np.testing.assert_array_equal(r1, r2)
+    assert s1["rays"] == s2["rays"] and s1["bvh_tests"] == s2["bvh_tests"], (s1, s2)
+    assert np.array_equal(a1.view(np.uint32), a2.view(np.uint32))
+
+
 @pytest.mark.parametrize("mode", ["linear", "stack_global"])
 def test_generated_stress_scene(have_gpu, tmp_path, monkeypatch, mode):
     """A scene from the authoring module (3000 random spheres, a 6 k-step threaded program; or the

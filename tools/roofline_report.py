@@ -60,17 +60,23 @@ def main(tag, name):
         if not os.path.exists(f):
             continue
         agg, names, dur = per_dispatch(f)
-        timed = [x for x in agg if ", false>" in names[x]]  # the product kernel's timed launch
+        # the product kernel's launches of the timed step (a step may be cut into several launches
+        # by the sample-buffer budget: counters and durations are summed over all of them, and the
+        # figures below are per average launch, like the bench's rays per launch)
+        timed = [x for x in agg if ", false>" in names[x]]
         if not timed:
             continue
-        disp = max(timed, key=lambda x: dur[x])
         line = bench_line(d + ".log")
-        r = line["detail"]["rays"] / max(1, line["detail"]["launches"])
+        launches = max(1, line["detail"]["launches"])
+        assert len(timed) == launches, (d, len(timed), launches)
+        r = line["detail"]["rays"] / launches
         if rays_per_launch is None:
             rays_per_launch = r
         assert abs(r - rays_per_launch) < 1, "passes disagree on rays per launch"
-        summary["pmc"].update(agg[disp])
-        summary["pmc_passes"][os.path.basename(d)] = {"dispatch_ms": dur[disp], "kernel": names[disp]}
+        for k in agg[timed[0]]:
+            summary["pmc"][k] = sum(agg[x][k] for x in timed) / launches
+        summary["pmc_passes"][os.path.basename(d)] = {"dispatch_ms": sum(dur[x] for x in timed) / launches,
+                                                      "dispatches": launches, "kernel": names[timed[0]]}
     p = summary["pmc"]
     summary["rays_per_launch"] = rays_per_launch
     per = {}
