@@ -607,11 +607,12 @@ bool CompileScene(const Scene& s, CompiledScene& out, std::string& err, bool acc
     for (size_t i = 0; i < n; i++)
       if (out.lin[4 * i] == kBvh || out.lin[4 * i] == kAccBvh || out.lin[4 * i] == kXform) target[out.lin[4 * i + 1]] = 1;
     for (size_t i = 0; i < n; i++) {
-      if (out.lin[4 * i] != kBvh) continue;
+      const uint32_t kind = out.lin[4 * i];
+      if (kind != kBvh && kind != kAccBvh) continue;  // accelerated-list tree nodes pair alike (padded boxes)
       uint32_t* w = &out.lin_wide[16 * i];
       w[2] = (uint32_t)(i + 1);
       w[3] = out.lin[4 * i + 1];
-      if (!pairs || second[i] || i + 1 >= n || out.lin[4 * (i + 1)] != kBvh || target[i + 1]) continue;
+      if (!pairs || second[i] || i + 1 >= n || out.lin[4 * (i + 1)] != kind || target[i + 1]) continue;
       const size_t c = i + 1;
       second[c] = 1;
       w[2] = (uint32_t)(c + 1);

@@ -118,6 +118,9 @@ constexpr int kBlock = 256;
 #ifndef RT2_BVH_SELECT
 #define RT2_BVH_SELECT 0  // threaded BVH step: branch-free next-index select (experiment)
 #endif
+#ifndef RT2_ACC_RUN
+#define RT2_ACC_RUN 1  // threaded program: accelerated-list tree steps join the BVH-step runs
+#endif
 #ifndef RT2_BVH_SPEC
 #define RT2_BVH_SPEC 0  // threaded BVH run: load step i + 1 while step i's slab test and wave minimum run
 #endif
@@ -1241,7 +1244,8 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
       }
     }
 #endif
-    if (sw[0] == kBvh) {
+#define RT2_IS_RUN(k) ((k) == kBvh || (RT2_ACC_RUN && RT2_WIDE_PROGRAM && Has<F, kFeatAccList>() && (k) == kAccBvh))
+    if (RT2_IS_RUN(sw[0])) {
       // A run of BVH steps in a loop of its own: only `next` changes from step to step, so nothing
       // else is carried (no register copies between kinds) and the step costs the slab test, the
       // next-index update and the wave-minimum search.
@@ -1256,6 +1260,30 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
         const uint32_t pi = i + 1u < len ? i + 1u : i;
         u32x16 spec;
         asm volatile("s_load_dwordx16 %0, %1, %2" : "=s"(spec) : "s"(P.lin_wide), "s"(pi * 64u));
+#endif
+#if RT2_ACC_RUN && RT2_WIDE_PROGRAM
+        if (Has<F, kFeatAccList>() && sw[0] == kAccBvh) {
+          if (next == i) {  // padded slab test of an accelerated list's tree node (as below)
+            if (kStats) cnt.bvh++;
+            const float ax = ((uf(sw[4]) - acc_pad) - o.x) * inv.x, bx = ((uf(sw[8]) + acc_pad) - o.x) * inv.x;
+            const float ay = ((uf(sw[5]) - acc_pad) - o.y) * inv.y, by = ((uf(sw[9]) + acc_pad) - o.y) * inv.y;
+            const float az = ((uf(sw[6]) - acc_pad) - o.z) * inv.z, bz = ((uf(sw[10]) + acc_pad) - o.z) * inv.z;
+            float t0, t1;
+            slab_t(ax, bx, ay, by, az, bz, tmin, tmax, t0, t1);
+            const bool in = t0 <= t1;
+            uint32_t nx = in ? i + 1u : sw[1];
+            if (sw[2] != i + 1u) {  // paired with its near child's step (compile.cpp), same tmax and padding
+              const float cx = ((uf(sw[7]) - acc_pad) - o.x) * inv.x, dx = ((uf(sw[13]) + acc_pad) - o.x) * inv.x;
+              const float cy = ((uf(sw[11]) - acc_pad) - o.y) * inv.y, dy = ((uf(sw[14]) + acc_pad) - o.y) * inv.y;
+              const float cz = ((uf(sw[12]) - acc_pad) - o.z) * inv.z, dz = ((uf(sw[15]) + acc_pad) - o.z) * inv.z;
+              float u0, u1;
+              slab_t(cx, dx, cy, dy, cz, dz, tmin, tmax, u0, u1);
+              if (kStats && in) cnt.bvh++;
+              nx = in ? (u0 <= u1 ? sw[2] : sw[3]) : sw[1];
+            }
+            next = nx;
+          }
+        } else
 #endif
 #if RT2_BVH_SELECT && RT2_WIDE_PROGRAM
         if (allfin) {  // every lane evaluates the slab test; the lanes at step i take its result
@@ -1323,7 +1351,7 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
           for (int j = 0; j < 8; j++) sw[4 + j] = b[j];
         }
 #endif
-      } while (sw[0] == kBvh);
+      } while (RT2_IS_RUN(sw[0]));
       if (i >= len) break;
     }
     const u32x4 st = {sw[0], sw[1], sw[2], sw[3]};
