@@ -95,7 +95,8 @@ constexpr int kBlock = 256;
 #define RT2_MIN_WAVES_VOL 7
 #endif
 #ifndef RT2_MIN_WAVES_B2LIN
-#define RT2_MIN_WAVES_B2LIN 7  // book 2 threaded: 3/4/5/6/7/8 waves 934/938/1091/1183/1297/508 Mray/s
+#define RT2_MIN_WAVES_B2LIN 8  // book 2 threaded (2000 spp): 6/7/8 waves 1685/1788/1887 Mray/s since its tree steps run in
+                               // the BVH-step loop (round 1, before: 3/4/5/6/7/8 waves 934/938/1091/1183/1297/508)
 #endif
 #ifndef RT2_MIN_WAVES_ALL
 #define RT2_MIN_WAVES_ALL 6
