@@ -61,3 +61,21 @@ def test_cpp_mirror_header_compiles():
     r = subprocess.run(["g++", "-std=c++17", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
                         "-fsyntax-only", src], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
+
+
+@pytest.mark.parametrize("scene,expect", [("book2_final_scene_10000_samples", 1), ("final_render_book_1", 1),
+                                          ("cornell_box_original", 0)])
+def test_paired_program_steps_are_well_formed(tmp_path, scene, expect):
+    """compile.cpp's paired BVH / list-tree steps (host only): a paired step precedes its near child,
+    carries that child's box and skip index, and no skip index lands on the child; sphere scenes
+    pair, the Cornell box does not (its kernel has no second test)."""
+    csrc = os.path.join(ROOT, "raytrace2_amd", "csrc")
+    exe = str(tmp_path / "program_pairs")
+    r = subprocess.run(["g++", "-O1", "-std=c++17", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include", "-I", csrc,
+                        "-o", exe, os.path.join(ROOT, "tests", "cpp", "program_pairs.cpp")]
+                       + [os.path.join(csrc, f) for f in ("json.cpp", "scene.cpp", "compile.cpp")],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
+    r = subprocess.run([exe, os.path.join(ROOT, "scenes", scene + ".json"), str(expect)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.startswith("pairs=")
