@@ -390,6 +390,7 @@ def main():
                        "per_rank": [{"rank": r["rank"], "rows": r["rows"], "mray_s": round(r["mray_s"], 1),
                                      "ms_per_step": round(r["elapsed_s"] * 1e3 / a.steps, 2),
                                      "kernel_ms_per_step": round(r["kernel_ms"] / a.steps, 2)} for r in per_rank],
+                       "runtime": R._native.runtime_info(),
                        "rays_per_sample": round(rays_total / (a.steps * a.spp * a.width *
                                                               sum(r["rows"] for r in per_rank)), 4)},
         }

@@ -188,6 +188,19 @@ RT2_API int rt2_tracer_gather(rt2_tracer* tr);
 RT2_API int rt2_tracer_image_accumulation(rt2_tracer* tr, float* out);        /* raw float3 sums */
 RT2_API int rt2_tracer_image_non_converted_pixels(rt2_tracer* tr, float* out); /* accum / frame_idx */
 RT2_API int rt2_tracer_image_pixels(rt2_tracer* tr, uint8_t* out_rgba);       /* Pixels(): RGBA8 */
+/* The gather's layout, for callers that move the band stacks themselves (e.g. over another
+ * collective library): every rank sends rt2_band_rows_max(height, band_h, world) rows of its band
+ * stack (padding rows zero); rt2_deinterleave_host turns the rank-major stacks
+ * [world][max_rows][width][channels] (what ncclGather delivers on the root) into the image
+ * [height][width][channels] on the host, with the same index map as the root's de-interleave
+ * kernel (rt2_layout.h BandSource). No GPU needed. */
+RT2_API int rt2_band_rows_max(int height, int band_h, int world);
+RT2_API int rt2_deinterleave_host(const float* stacks, float* image, int width, int height, int band_h, int world,
+                                  int max_rows, int channels);
+/* The RCCL and HIP runtime this process runs (the first library of each name loaded wins: under
+ * PyTorch that is torch's bundled copy, in a plain C++ process the one librt2.so was linked with):
+ * writes "rccl <version> <path>; hip <path>" into out. */
+RT2_API int rt2_runtime_info(char* out, size_t cap);
 
 RT2_API int rt2_tracer_enable_ray_counts(rt2_tracer* tr, int on);
 RT2_API int rt2_tracer_ray_counts(rt2_tracer* tr, uint32_t* out); /* rays per local pixel */

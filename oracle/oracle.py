@@ -64,6 +64,9 @@ def lib():
         L.oracle_sphere_hit.argtypes = [fp, fp]
         L.oracle_aabb_hit.argtypes = [fp]
         L.oracle_transform.argtypes = [fp, fp, fp]
+        L.oracle_set_controls.argtypes = [i32]
+        L.oracle_set_controls.restype = None
+        L.oracle_get_controls.restype = i32
         L.oracle_render.argtypes = [vp, i32, i32, i32, i32, u64, i32, i32, i32, i32, i32, fp,
                                     ctypes.POINTER(ctypes.c_uint32), i32, i32, ctypes.POINTER(Counters)]
         _lib = L
@@ -150,6 +153,29 @@ class OracleScene:
         lib().oracle_render(self._h, w, h, spp_setting, max_depth, seed, frame_begin, frames, band_h, rank, world,
                             _f(accum), _u(ray_counts), threads, 1 if forward else 0, ctypes.byref(cnt))
         return accum, ray_counts, cnt.as_dict()
+
+
+# Controls that REMOVE one reference quirk each (rt_oracle.cpp g_controls): tests of the power of
+# the screenshot pins only. 0 = the faithful restatement.
+CTL_WORLD_T = 1      # transformed children report world-space t (Transform.cpp:13-20,75-88 quirk removed)
+CTL_SINGLE_LEAF = 2  # span-1 BVH leaves tested once (BVH.cpp:18-20,50-55 quirk removed)
+CTL_INF = 4          # kInfinity = +inf instead of FLT_MAX (Defs.hpp:17)
+
+
+class controls:
+    """Context manager: scenes loaded and rendered inside it use the given control mask."""
+
+    def __init__(self, mask: int):
+        self.mask = mask
+
+    def __enter__(self):
+        self.prev = lib().oracle_get_controls()
+        lib().oracle_set_controls(self.mask)
+        return self
+
+    def __exit__(self, *exc):
+        lib().oracle_set_controls(self.prev)
+        return False
 
 
 def philox(ctr, key):

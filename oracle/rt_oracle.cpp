@@ -45,7 +45,16 @@
 namespace oracle {
 
 using real = float;
-constexpr real kInfinity = FLT_MAX;  // Defs.hpp:17
+// Controls (tests only, oracle_set_controls): each bit REMOVES one of the reference's quirks, to
+// measure whether the statistical pins against the reference's screenshots can tell the faithful
+// restatement from one without that quirk (DESIGN.md §2 "Power of the pin"). 0 = faithful.
+//   1: transformed children report world-space t (model-space direction left unnormalised) instead
+//      of the model-space t of Transform.cpp:13-20,75-88
+//   2: a span-1 BVH leaf is tested once, not twice (BVH.cpp:18-20, 50-55)
+//   4: kInfinity = +inf instead of FLT_MAX (Defs.hpp:17)
+enum : int { kCtlWorldT = 1, kCtlSingleLeaf = 2, kCtlInf = 4 };
+static int g_controls = 0;
+#define kInfinity ((g_controls & kCtlInf) ? (real)INFINITY : (real)FLT_MAX)  // Defs.hpp:17
 
 // ----------------------------------------------------------------------------------------------
 // glm-like value types (Appendix C of SURVEY.md). Column-major mat4 like glm.
@@ -304,7 +313,7 @@ struct Interval {
     return {min - padding, max + padding};
   }
 };
-const Interval kUniverse{-kInfinity, kInfinity};
+#define kUniverse (Interval{-kInfinity, kInfinity})
 
 struct Ray {
   vec3 origin, direction;
@@ -534,7 +543,8 @@ struct Transformed : Hittable {
   }
   Ray WorldToModel(const Ray& r) const {
     vec3 o = xyz(mul(inv_model, vec4{r.origin.x, r.origin.y, r.origin.z, 1}));
-    vec3 d = normalize(mul3(inv_model, r.direction));
+    vec3 d = mul3(inv_model, r.direction);
+    if (!(g_controls & kCtlWorldT)) d = normalize(d);  // Transform.cpp:17: the quirk (model-space t)
     return Ray{o, d, r.time};
   }
   bool Hit(Ctx& c, const Ray& r, Interval ray_t, HitRecord& rec) const override {
@@ -608,6 +618,7 @@ struct BVHNode : Hittable {
     c.cnt->bvh++;
     if (!aabb.Hit(r, ray_t)) return false;
     bool hit_left = left->Hit(c, r, ray_t, rec);
+    if ((g_controls & kCtlSingleLeaf) && left == right) return hit_left;
     bool hit_right = right->Hit(c, r, Interval(ray_t.min, hit_left ? rec.t : ray_t.max), rec);
     return hit_left || hit_right;
   }
@@ -1281,6 +1292,10 @@ struct oracle_scene_info {
 static thread_local std::string g_err;
 
 const char* oracle_last_error() { return g_err.c_str(); }
+
+// Test controls (see g_controls); set before loading a scene (AABB defaults use kInfinity).
+void oracle_set_controls(int mask) { g_controls = mask; }
+int oracle_get_controls() { return g_controls; }
 
 void* oracle_scene_load(const char* path, uint64_t seed) {
   std::string err;

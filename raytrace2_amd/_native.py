@@ -148,6 +148,9 @@ def _load():
         "rt2_tracer_image_non_converted_pixels": (i32, [vp, fp]),
         "rt2_tracer_image_pixels": (i32, [vp, ctypes.POINTER(ctypes.c_uint8)]),
         "rt2_selftest": (i32, [i32, i32, u64, u64, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
+        "rt2_band_rows_max": (i32, [i32, i32, i32]),
+        "rt2_deinterleave_host": (i32, [fp, fp, i32, i32, i32, i32, i32, i32]),
+        "rt2_runtime_info": (i32, [ctypes.c_char_p, ctypes.c_size_t]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -171,3 +174,10 @@ def selftest(which: int, n: int, seed: int = 1, device: int = 0):
     bad, checked = ctypes.c_uint64(0), ctypes.c_uint64(0)
     check(lib.rt2_selftest(device, which, n, seed, ctypes.byref(bad), ctypes.byref(checked)))
     return bad.value, checked.value
+
+
+def runtime_info() -> str:
+    """rt2_runtime_info: the RCCL (version, path) and HIP runtime library this process runs."""
+    buf = ctypes.create_string_buffer(1024)
+    check(lib.rt2_runtime_info(buf, len(buf)))
+    return buf.value.decode(errors="replace")

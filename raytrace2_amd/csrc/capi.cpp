@@ -5,7 +5,10 @@
 #include <hip/hip_runtime_api.h>
 #include <rccl/rccl.h>
 
+#include <dlfcn.h>
+
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -95,11 +98,15 @@ struct rt2_tracer {
   bool frame_tiles = false;                // this launch: items = one pixel x 64 short chunks per wave
   int frame_tile_len = 8;                  // most frames per chunk in frame-tile mode (RT2_FRAME_TILE_LEN)
   bool chunk_align = true;                 // chunks of >= kOctet frames: multiples of 4 frames
-  uint32_t* d_chunks = nullptr;            // chunk table of the last launch shape (ChunkSchedule)
+  uint32_t* d_chunks = nullptr;            // chunk tables of the last render's launches (ChunkSchedule)
   size_t chunks_bytes = 0;
-  uint32_t n_chunks = 0;
-  int first_chunk_frames = 0;
-  uint64_t chunk_key[6] = {~0ull, 0, 0, 0, 0, 0};
+  std::vector<uint32_t> chunks_host;       // what d_chunks holds (renders repeat one schedule: no upload)
+  struct Staging {                         // pinned host copies of uploaded tables, reusable once copied
+    uint32_t* p;
+    size_t bytes;
+    hipEvent_t done;
+  };
+  std::vector<Staging> staging;
   int batch_max = 64;                      // most work items a wave reserves with one atomic
   int last_chunk_frames = 0;
   int occ_key = -1, occ_blocks = 1;  // cached occupancy of the last kernel instantiation
@@ -167,14 +174,12 @@ int BandH(const rt2_tracer* t) { return t->band_h > 0 ? t->band_h : (t->height >
 
 // Rows of the largest rank's band stack (every rank's accumulation is allocated this tall, so the
 // gather sends equal counts; the padding rows stay zero).
-int BandRowsMax(const rt2_tracer* t) {
-  if (t->height <= 0) return 0;
-  const int bh = BandH(t);
-  const int bands = (t->height + bh - 1) / bh;
-  return (bands + t->world - 1) / t->world * bh;
-}
+int BandRowsMax(const rt2_tracer* t) { return rt2::BandRowsMax(t->height, t->band_h, t->world); }
 
-int AllocRows(const rt2_tracer* t) { return t->world > 1 ? BandRowsMax(t) : t->local_rows; }
+// Rows of the accumulation buffer: the gather sends BandRowsMax rows from every rank, also at world 1
+// (a band height that does not divide the image height leaves padding rows), so every buffer is that
+// tall; the rows past local_rows stay zero.
+int AllocRows(const rt2_tracer* t) { return BandRowsMax(t); }
 
 void FreeImage(rt2_tracer* t) {
   (void)hipFree(t->d_stacks);
@@ -189,7 +194,7 @@ void FreeImage(rt2_tracer* t) {
 }
 
 void FreeFrame(rt2_tracer* t) {
-  (void)hipFree(t->d_samples);
+  if (t->d_samples) (void)hipFreeAsync(t->d_samples, t->stream);  // stream-ordered (LaunchFrames)
   t->d_samples = nullptr;
   t->samples_bytes = 0;
   (void)hipFree(t->d_accum);
@@ -566,7 +571,12 @@ void rt2_tracer_destroy(rt2_tracer* t) {
   (void)hipFree(t->d_lind);
   (void)hipFree(t->d_work);
   (void)hipFree(t->d_stats);
-  (void)hipFree(t->d_chunks);
+  if (t->d_chunks) (void)hipFreeAsync(t->d_chunks, t->stream);
+  if (t->stream) (void)hipStreamSynchronize(t->stream);
+  for (auto& st : t->staging) {
+    (void)hipEventDestroy(st.done);
+    (void)hipHostFree(st.p);
+  }
   if (t->own_stream) (void)hipStreamDestroy(t->own_stream);
   delete t;
 }
@@ -766,17 +776,14 @@ Magic MakeMagic(uint32_t d) {  // rt2_layout.h Magic: floor(n / d) for n < 2^31
 // items per chunk, L = resident lanes, k = work_split), at least 1 and at most chunk_max: early
 // items are long (few item setups per sample) and the last ones short, so the launch's tail — the
 // time in which lanes run out of work while others finish their item — stays short. k = 0: one
-// chunk (each pixel's frames in one item). Cached: the bench repeats one launch shape.
-int ChunkSchedule(rt2_tracer* t, int fb, int n, uint32_t tile_items, int64_t lanes, int sq) {
-  const uint64_t key[6] = {(uint64_t)fb, (uint64_t)n, tile_items, (uint64_t)lanes,
-                           (uint64_t)t->work_split | ((uint64_t)t->chunk_max << 32) | ((uint64_t)t->chunk_align << 63) |
-                               ((uint64_t)t->frame_tiles << 62),
-                           (uint64_t)sq | ((uint64_t)t->frame_tile_len << 32)};
-  if (t->d_chunks && memcmp(key, t->chunk_key, sizeof(key)) == 0) return RT2_OK;
+// chunk (each pixel's frames in one item). Appends the table (first frame, stratum) per chunk and
+// the sentinel to `tab`; returns the number of chunks and the first chunk's length.
+void ChunkSchedule(const rt2_tracer* t, int fb, int n, uint32_t tile_items, int64_t lanes, int sq,
+                   std::vector<uint32_t>& tab, uint32_t* n_chunks, int* first_len) {
+  const size_t start = tab.size();
   // items must stay below 2^31 (kernel index arithmetic): shortest chunk that allows it
   const int64_t max_chunks = std::max<int64_t>(1, (int64_t)0x7FFFFFFF / tile_items);
   const int lo = (int)std::max<int64_t>(1, ((int64_t)n + max_chunks - 1) / max_chunks);
-  std::vector<uint32_t> tab;
   int first = 0;
   // frame tiles: chunks of up to frame_tile_len frames, as even as the 64-chunk groups allow (the
   // last group is padded with empty chunks, whose lanes fetch again)
@@ -805,28 +812,57 @@ int ChunkSchedule(rt2_tracer* t, int fb, int n, uint32_t tile_items, int64_t lan
     s += len;
   }
   if (t->frame_tiles) {  // padding chunks up to a multiple of 64 (empty: first frame = the launch end)
-    while ((tab.size() / 2) % 64 != 0) {
+    while (((tab.size() - start) / 2) % 64 != 0) {
       tab.push_back((uint32_t)(fb + n));
       tab.push_back(0u);
     }
   }
   tab.push_back((uint32_t)(fb + n));
   tab.push_back(0u);
+  *n_chunks = (uint32_t)((tab.size() - start) / 2 - 1);
+  *first_len = first;
+}
+
+// Puts a render's chunk tables in d_chunks, ordered on the tracer's stream: the copy runs after the
+// launches already queued there (which may still read the old tables), from pinned staging memory,
+// so the host never waits for the GPU (a multi-GPU tracer enqueues every GPU's launches at once).
+// A render repeating the last schedule (the bench, a progressive loop's steady state) uploads nothing.
+int UploadChunks(rt2_tracer* t, const std::vector<uint32_t>& tab) {
+  if (t->d_chunks && tab == t->chunks_host) return RT2_OK;
   const size_t bytes = tab.size() * sizeof(uint32_t);
   if (bytes > t->chunks_bytes) {
-    HIP_TRY(hipStreamSynchronize(t->stream));  // the old table may still be read
-    (void)hipFree(t->d_chunks);
+    // grow geometrically; stream-ordered free and allocation: the queued launches that read the old
+    // tables run first, and the host does not wait (hipFree would synchronize the device)
+    const size_t cap = std::max(bytes, 2 * t->chunks_bytes);
+    if (t->d_chunks) HIP_TRY(hipFreeAsync(t->d_chunks, t->stream));
     t->d_chunks = nullptr;
     t->chunks_bytes = 0;
-    HIP_TRY(hipMalloc(&t->d_chunks, bytes));
-    t->chunks_bytes = bytes;
-  } else if (t->d_chunks) {
-    HIP_TRY(hipStreamSynchronize(t->stream));
+    t->chunks_host.clear();
+    HIP_TRY(hipMallocAsync((void**)&t->d_chunks, cap, t->stream));
+    t->chunks_bytes = cap;
   }
-  HIP_TRY(hipMemcpy(t->d_chunks, tab.data(), bytes, hipMemcpyHostToDevice));
-  t->n_chunks = (uint32_t)(tab.size() / 2 - 1);
-  t->first_chunk_frames = first;
-  memcpy(t->chunk_key, key, sizeof(key));
+  // a staging buffer whose previous copy has run, else a new one
+  rt2_tracer::Staging* st = nullptr;
+  for (auto& c : t->staging) {
+    if (c.bytes < bytes) continue;
+    const hipError_t q = hipEventQuery(c.done);
+    if (q == hipSuccess) {
+      st = &c;
+      break;
+    }
+    if (q != hipErrorNotReady) return HipFail(q, "hipEventQuery");
+  }
+  if (!st) {
+    rt2_tracer::Staging c{nullptr, std::max<size_t>(bytes, 4096), nullptr};
+    HIP_TRY(hipHostMalloc((void**)&c.p, c.bytes, hipHostMallocDefault));
+    HIP_TRY(hipEventCreateWithFlags(&c.done, hipEventDisableTiming));
+    t->staging.push_back(c);
+    st = &t->staging.back();
+  }
+  memcpy(st->p, tab.data(), bytes);
+  HIP_TRY(hipMemcpyAsync(t->d_chunks, st->p, bytes, hipMemcpyHostToDevice, t->stream));
+  HIP_TRY(hipEventRecord(st->done, t->stream));
+  t->chunks_host = tab;
   return RT2_OK;
 }
 
@@ -866,6 +902,8 @@ int LaunchFrames(rt2_tracer* t, int n_frames) {
   p.div_band_w = MakeMagic((uint32_t)p.band_h * (uint32_t)p.world);
   p.div_world = MakeMagic((uint32_t)p.world);
   p.local_pixels = (uint32_t)t->width * (uint32_t)t->local_rows;
+  if (p.tile_items > 0x7FFFFFFFu)  // work items (and pixel indices) must stay below 2^31
+    return Fail(RT2_ERR_INVALID, "image too large for one GPU (more than 2^31 pixels in a partition)");
   p.max_depth = t->max_depth;
   p.seed_lo = (uint32_t)t->seed;
   p.seed_hi = (uint32_t)(t->seed >> 32);
@@ -883,6 +921,8 @@ int LaunchFrames(rt2_tracer* t, int n_frames) {
   // up to 8 frames, book 2 (4,922 steps) +4 %, book 1 (995 steps) +4.5 %; Cornell (29 steps) -2 %,
   // where 8x8 pixel tiles are as coherent and the shorter chunks cost more item fetches.
   t->frame_tiles = t->frame_tiles_env >= 0 ? t->frame_tiles_env == 1 : (p.lin_len > kFrameTileMinSteps);
+  // frame-tile items are g * 64 * local_pixels + ...: at least one 64-chunk group must stay below 2^31
+  if ((uint64_t)p.local_pixels * 64u > 0x7FFFFFFFull) t->frame_tiles = false;
   uint32_t feats = t->features | (p.cam.defocus_angle > 0.0f ? (uint32_t)kFeatDefocus : 0u);
   int variant = RenderVariant(feats);
   // per-record counters and per-pixel ray counts come from the counting kernel instantiation (same
@@ -945,41 +985,58 @@ int LaunchFrames(rt2_tracer* t, int n_frames) {
   if (need > t->samples_bytes) {
     // grow geometrically (progressive loops raise their frames per call a little at a time)
     need = std::max(need, std::min(2 * t->samples_bytes, octets(budget_frames) * frame_bytes));
-    HIP_TRY(hipStreamSynchronize(t->stream));  // the old buffer may still be read
-    (void)hipFree(t->d_samples);
+    // stream-ordered: the queued launches still using the old buffer run first; the host does not
+    // wait (a multi-GPU tracer enqueues every GPU's render before any of them finishes)
+    if (t->d_samples) HIP_TRY(hipFreeAsync(t->d_samples, t->stream));
     t->d_samples = nullptr;
     t->samples_bytes = 0;
-    HIP_TRY(hipMalloc(&t->d_samples, need));
+    HIP_TRY(hipMallocAsync((void**)&t->d_samples, need, t->stream));
     t->samples_bytes = need;
   }
   p.samples = t->d_samples;
   t->last_variant = variant;
-  for (int done = 0; done < n_frames; done += p.n_frames) {
-    p.frame_begin = (int)t->frame_idx;
-    p.n_frames = std::min(per_launch, n_frames - done);
+  // every launch's chunk table first (one stream-ordered upload), then the launches
+  struct Launch {
+    int frame_begin, n_frames, first_len;
+    uint32_t n_chunks;
+    size_t table;  // offset in `tabs` (words)
+  };
+  std::vector<Launch> launches;
+  std::vector<uint32_t> tabs;
+  for (int done = 0, fb = (int)t->frame_idx; done < n_frames;) {
+    Launch L{fb, std::min(per_launch, n_frames - done), 0, 0, tabs.size()};
     // Split each pixel's frames into chunks so that the launch has about work_split items per
     // resident lane: a persistent lane's last item is then short, and a small partition (a row
     // band of an 8-GPU split) still fills every CU. Samples land in the per-frame buffer, so the
     // accumulation order does not depend on the split.
-    int rc = ChunkSchedule(t, p.frame_begin, p.n_frames, p.tile_items, resident, p.cam.sqrt_spp);
-    if (rc != RT2_OK) return rc;
-    p.chunks = t->d_chunks;
-    p.n_chunks = t->n_chunks;
+    ChunkSchedule(t, L.frame_begin, L.n_frames, p.tile_items, resident, p.cam.sqrt_spp, tabs, &L.n_chunks,
+                  &L.first_len);
+    launches.push_back(L);
+    done += L.n_frames;
+    fb += L.n_frames;
+  }
+  int rc = UploadChunks(t, tabs);
+  if (rc != RT2_OK) return rc;
+  for (const Launch& L : launches) {
+    p.frame_begin = L.frame_begin;
+    p.n_frames = L.n_frames;
+    p.chunks = t->d_chunks + L.table;
+    p.n_chunks = L.n_chunks;
     if (t->frame_tiles) {
       p.frame_tiles = 1u;
       p.frame_tile = 64u * p.local_pixels;
       p.div_frame_tile = MakeMagic(p.frame_tile);
       p.div_width = MakeMagic((uint32_t)t->width);
-      p.n_items = (t->n_chunks / 64u) * p.frame_tile;
+      p.n_items = (L.n_chunks / 64u) * p.frame_tile;
     } else {
-      p.n_items = t->n_chunks * p.tile_items;
+      p.n_items = L.n_chunks * p.tile_items;
     }
     p.batch_max = (uint32_t)t->batch_max;
     p.batch_div = (uint32_t)std::max<int64_t>(1, (resident / 64) * 2);  // half of the left work / waves
     int grid = (int)std::min<int64_t>(resident, (int64_t)p.n_items) / RenderBlockSize();
     grid = std::max(grid, 1);
     t->last_grid = grid;
-    t->last_chunk_frames = t->first_chunk_frames;
+    t->last_chunk_frames = L.first_len;
     HIP_TRY(hipMemsetAsync(t->d_work, 0, sizeof(uint32_t), t->stream));
     hipEvent_t e0 = TakeEvent(t), e1 = TakeEvent(t);
     if (e0) HIP_TRY(hipEventRecord(e0, t->stream));
@@ -1056,6 +1113,17 @@ int GatherRanks(const std::vector<rt2_tracer*>& ranks, bool loopback) {
         }
         HIP_TRY(hipMemcpyAsync(root->d_stacks + (size_t)p->rank * count, p->d_accum, count * sizeof(float),
                                hipMemcpyDeviceToDevice, root->stream));
+      }
+      // later work on a part's stream (Render, Reset) must not overwrite its accumulation while the
+      // root's copy may still read it: every part stream waits for the copies
+      if (ranks.size() > 1) {
+        HIP_TRY(hipSetDevice(root->device));
+        hipEvent_t e = TakeEvent(root);
+        if (!e) return Fail(RT2_ERR_HIP, "event create failed");
+        HIP_TRY(hipEventRecord(e, root->stream));
+        for (rt2_tracer* p : ranks)
+          if (p != root) HIP_TRY(hipStreamWaitEvent(p->stream, e, 0));
+        root->event_pool.push_back(e);
       }
     } else {
       for (rt2_tracer* p : ranks)
@@ -1508,6 +1576,40 @@ int rt2_tracer_reset_stats(rt2_tracer* t) {
   t->kernel_ms = 0;
   t->gathers = 0;
   t->gather_ms = 0;
+  return RT2_OK;
+}
+
+int rt2_band_rows_max(int height, int band_h, int world) {
+  if (height < 0 || band_h < 0 || world < 1) return Fail(RT2_ERR_INVALID, "bad band layout");
+  return rt2::BandRowsMax(height, band_h, world);
+}
+
+int rt2_deinterleave_host(const float* stacks, float* image, int width, int height, int band_h, int world,
+                          int max_rows, int channels) {
+  if (!stacks || !image || width < 0 || height < 0 || band_h < 0 || world < 1 || channels < 1)
+    return Fail(RT2_ERR_INVALID, "bad de-interleave arguments");
+  if (max_rows < rt2::BandRowsMax(height, band_h, world))
+    return Fail(RT2_ERR_INVALID, "max_rows is below the largest rank's band stack");
+  const size_t row = (size_t)width * (size_t)channels;
+  for (int y = 0; y < height; y++) {
+    const BandRow src = BandSource(y, band_h, world);
+    memcpy(image + (size_t)y * row, stacks + ((size_t)src.rank * (size_t)max_rows + (size_t)src.row) * row,
+           row * sizeof(float));
+  }
+  return RT2_OK;
+}
+
+int rt2_runtime_info(char* out, size_t cap) {
+  if (!out || cap == 0) return Fail(RT2_ERR_INVALID, "null argument");
+  int v = 0;
+  (void)ncclGetVersion(&v);
+  auto path_of = [](const void* sym) {
+    Dl_info di;
+    return dladdr(sym, &di) && di.dli_fname ? std::string(di.dli_fname) : std::string("?");
+  };
+  const std::string s = "rccl " + std::to_string(v) + " " + path_of((const void*)&ncclGetVersion) + "; hip " +
+                        path_of((const void*)&hipGetDeviceCount);
+  snprintf(out, cap, "%s", s.c_str());
   return RT2_OK;
 }
 

@@ -10,6 +10,8 @@
 
 #include <cstdint>
 
+#include "rt2_layout.h"
+
 namespace rt2 {
 namespace dev {
 
@@ -25,11 +27,8 @@ __global__ __launch_bounds__(256) void deinterleave_kernel(const float* __restri
   const uint32_t i = blockIdx.x * 256u + threadIdx.x;
   if (i >= npix) return;
   const uint32_t y = i / width, x = i - y * width;
-  const uint32_t band = y / band_h;
-  const uint32_t period = band / world;
-  const uint32_t rank = (band - period * world + period) % world;  // rt2_layout.h BandRank
-  const uint32_t row = period * band_h + (y - band * band_h);       // rank-local row
-  const float* s = stacks + 3ull * (((unsigned long long)rank * max_rows + row) * width + x);
+  const BandRow src = BandSource((int)y, (int)band_h, (int)world);  // rt2_layout.h
+  const float* s = stacks + 3ull * (((unsigned long long)src.rank * max_rows + (uint32_t)src.row) * width + x);
   const float a0 = s[0], a1 = s[1], a2 = s[2];
   image[3ull * i] = a0;
   image[3ull * i + 1] = a1;

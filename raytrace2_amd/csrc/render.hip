@@ -43,22 +43,8 @@ namespace dev {
 
 constexpr int kBlock = 256;
 
-// Ablation switches for performance experiments only (tools/ablate.sh); all default off.
-#ifndef RT2_EXP_NO_BALLOT
-#define RT2_EXP_NO_BALLOT 0
-#endif
-#ifndef RT2_EXP_CHEAP_RNG
-#define RT2_EXP_CHEAP_RNG 0
-#endif
-#ifndef RT2_EXP_FAST_DIV
-#define RT2_EXP_FAST_DIV 0
-#endif
-#ifndef RT2_EXP_NO_FIN_AABB
-#define RT2_EXP_NO_FIN_AABB 0  // ablation: always the reference-order slab test
-#endif
-#ifndef RT2_EXP_NO_UNIT_QUAD
-#define RT2_EXP_NO_UNIT_QUAD 0  // ablation: unit-normal quads take the general axis-aligned test
-#endif
+// Diagnostic builds (tools/: cost probes, wave-step counts, section times, launch-tail times); all
+// default off. The product kernel is the build with none of them.
 #ifndef RT2_EXP_TRACE_TWICE
 #define RT2_EXP_TRACE_TWICE 0  // cost probe: every ray is traced a second time (result discarded)
 #endif
@@ -75,16 +61,7 @@ constexpr int kBlock = 256;
 #ifndef RT2_EXP_ENDTIME
 #define RT2_EXP_ENDTIME 0  // diagnostic build: per-wave start / first-idle / end times (s_memrealtime) into diag
 #endif
-#ifndef RT2_QUAD_PREFETCH
-#define RT2_QUAD_PREFETCH 0  // threaded program: touch the next quad record of a run early (measured slower:
-                             // Cornell 28.1 -> 26.7, book 2 1.45 -> 1.43 Grays/s)
-#endif
-#ifndef RT2_WIDE_PROGRAM
-#define RT2_WIDE_PROGRAM 1  // threaded program: 64-byte steps (entry + first 48 record bytes, one load)
-#endif
-#ifndef RT2_RARE_MIN
-#define RT2_RARE_MIN 0  // stack traversal: lanes needed before a rare, expensive step kind runs (0: off)
-#endif
+// Occupancy targets (waves per SIMD) per kernel variant; overridable for sweeps (tools/build_variants.sh).
 #ifndef RT2_MIN_WAVES_CORNELL
 #define RT2_MIN_WAVES_CORNELL 8
 #endif
@@ -103,30 +80,6 @@ constexpr int kBlock = 256;
 #endif
 #ifndef RT2_MIN_WAVES_PER_EU
 #define RT2_MIN_WAVES_PER_EU 0  // 0: per-variant occupancy targets (kMinWaves below)
-#endif
-#ifndef RT2_KARG
-#define RT2_KARG 1  // launch constants re-read from the kernel-argument segment at their uses (see karg16)
-#endif
-#ifndef RT2_KARG_CAMERA
-#define RT2_KARG_CAMERA RT2_KARG
-#endif
-#ifndef RT2_LDS_RNG
-#define RT2_LDS_RNG 1  // threaded kernels: the lane's Philox block in LDS rather than live VGPRs
-#endif
-#ifndef RT2_RAW_MINMAX
-#define RT2_RAW_MINMAX 1  // slab tests: single v_min/v_max instructions (no operand quieting)
-#endif
-#ifndef RT2_BVH_SELECT
-#define RT2_BVH_SELECT 0  // threaded BVH step: branch-free next-index select (experiment)
-#endif
-#ifndef RT2_ACC_RUN
-#define RT2_ACC_RUN 1  // threaded program: accelerated-list tree steps join the BVH-step runs
-#endif
-#ifndef RT2_BVH_SPEC
-#define RT2_BVH_SPEC 0  // threaded BVH run: load step i + 1 while step i's slab test and wave minimum run
-#endif
-#ifndef RT2_OCTET_STAGE
-#define RT2_OCTET_STAGE 1  // threaded kernels at <= 7 waves: stage a lane's samples in LDS, one 96-B store per octet
 #endif
 
 extern __shared__ float4 s_dyn[];  // [lds_nodes scene records][stack_depth * kBlock stack words]
@@ -242,12 +195,6 @@ __device__ __forceinline__ uint32_t sld1(const void* base, uint32_t off) {
   asm("s_load_dword %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(base), "s"(off));
   return v;
 }
-__device__ __forceinline__ u32x4 sld4(const void* base, uint32_t off) {
-  off = __builtin_amdgcn_readfirstlane(off);
-  u32x4 v;
-  asm("s_load_dwordx4 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(base), "s"(off));
-  return v;
-}
 __device__ __forceinline__ u32x8 sld8(const void* base, uint32_t off) {
   off = __builtin_amdgcn_readfirstlane(off);
   u32x8 v;
@@ -260,13 +207,6 @@ __device__ __forceinline__ u32x16 sld16(const void* base, uint32_t off) {
   asm("s_load_dwordx16 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(base), "s"(off));
   return v;
 }
-// Software prefetch into the scalar cache: a one-dword load left in flight into `dst`, which stays
-// reserved until sld_wait1(dst) has completed it.
-__device__ __forceinline__ void sld_touch(const void* base, uint32_t off, uint32_t& dst) {
-  off = __builtin_amdgcn_readfirstlane(off);
-  asm volatile("s_load_dword %0, %1, %2" : "=s"(dst) : "s"(base), "s"(off));
-}
-__device__ __forceinline__ void sld_wait1(uint32_t& v) { asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(v)); }
 // 20 dwords (one quad record) at off
 __device__ __forceinline__ void sld20(const void* base, uint32_t off, u32x16& a, u32x4& b) {
   off = __builtin_amdgcn_readfirstlane(off);
@@ -394,10 +334,6 @@ struct ShadeArgs {
   const float4* perlin_vec;
   const int* perlin_perm;
 };
-__device__ __forceinline__ ShadeArgs shade_args_of(const RenderParams& P) {
-  return ShadeArgs{reinterpret_cast<const float4*>(P.materials), reinterpret_cast<const float4*>(P.textures),
-                   reinterpret_cast<const float4*>(P.perlin_vec), P.perlin_perm};
-}
 __device__ __forceinline__ ShadeArgs shade_args() {
   static_assert(RT2_KOFF(materials) == 8 && RT2_KOFF(perlin_perm) == 32, "RenderParams layout");
   const u32x8 v = karg8<8>();
@@ -406,25 +342,6 @@ __device__ __forceinline__ ShadeArgs shade_args() {
                    reinterpret_cast<const float4*>(ptr(4)), reinterpret_cast<const int*>(ptr(6))};
 }
 
-// The same launch constants read from the kernel argument as the compiler sees fit (RT2_KARG 0).
-__device__ __forceinline__ LoopArgs loop_args_of(const RenderParams& P) {
-  LoopArgs r;
-  const uint32_t* w = reinterpret_cast<const uint32_t*>(&P);
-#pragma unroll
-  for (int k = 0; k < 16; k++) {
-    r.a[k] = w[LoopArgs::kA / 4 + k];
-    r.b[k] = w[LoopArgs::kB / 4 + k];
-  }
-  r.w = (uint32_t)P.width;
-  return r;
-}
-#if RT2_KARG
-#define RT2_LOOP_ARGS() loop_args()
-#define RT2_SHADE_ARGS() shade_args()
-#else
-#define RT2_LOOP_ARGS() loop_args_of(P)
-#define RT2_SHADE_ARGS() shade_args_of(P)
-#endif
 
 // Philox keys and the image width (the stream's pixel index), one wait.
 __device__ __forceinline__ void seed_args(uint32_t& k0, uint32_t& k1, uint32_t& width) {
@@ -451,7 +368,7 @@ __device__ __forceinline__ void philox(uint32_t k0, uint32_t k1, uint32_t pixel,
   asm volatile("" : "+s"(key0), "+s"(key1));
   const uint32_t m0 = 0xD2511F53u, m1 = 0xCD9E8D57u;
 #pragma unroll
-  for (int r = 0; r < (RT2_EXP_CHEAP_RNG ? 2 : 10); r++) {
+  for (int r = 0; r < 10; r++) {
     // one v_mad_u64_u32 gives both halves of each 32x32 product; xor3 is one v_bitop3_b32
     uint64_t p0, p1;
     asm("v_mad_u64_u32 %0, vcc, %1, %2, 0" : "=v"(p0) : "s"(m0), "v"(c0) : "vcc");
@@ -481,7 +398,6 @@ __device__ __forceinline__ float to_unit(uint32_t v) { return (float)(v >> 8) * 
 // of four VGPRs that stay live across the whole render loop.
 template <bool kLdsRng>
 struct PathT {
-  uint32_t k0, k1, width;  // wave-uniform: seed, image width
   uint32_t frame;
   uint32_t xy;   // pixel x | y << 16 (global image coordinates)
   uint32_t sij;  // stratum s_i | s_j << 16 of `frame` (RayTracer.cpp:59-60), advanced per frame
@@ -493,13 +409,9 @@ struct PathT {
     n = 0;  // buffer holds block -1: the first group refills
   }
   __device__ __forceinline__ void block(uint32_t b, uint32_t& w0, uint32_t& w1, uint32_t& w2, uint32_t& w3) const {
-#if RT2_KARG
     uint32_t key0, key1, w;
     seed_args(key0, key1, w);  // re-read at the refill (see karg16)
     philox(key0, key1, (xy >> 16) * w + (xy & 0xFFFFu), frame, b, w0, w1, w2, w3);
-#else
-    philox(k0, k1, (xy >> 16) * width + (xy & 0xFFFFu), frame, b, w0, w1, w2, w3);
-#endif
   }
   // K consecutive uniforms in [0,1) (24-bit mantissa), in stream order
   template <int K>
@@ -640,7 +552,6 @@ __device__ __forceinline__ bool aabb_hit(float4 lo, float4 hi, f3 o, f3 inv, flo
 // VALU operation or is a finite record bound, so it is never a signalling NaN, and v_min_f32 /
 // v_max_f32 already return the other operand for a quiet NaN: the same values, minNum / maxNum
 // semantics included (the padded slab test relies on NaN being ignored).
-#if RT2_RAW_MINMAX
 __device__ __forceinline__ float vmin(float a, float b) {
   float r;
   asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
@@ -661,12 +572,6 @@ __device__ __forceinline__ float vmax3(float a, float b, float c) {
   asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
   return r;
 }
-#else
-__device__ __forceinline__ float vmin(float a, float b) { return fminf(a, b); }
-__device__ __forceinline__ float vmax(float a, float b) { return fmaxf(a, b); }
-__device__ __forceinline__ float vmin3(float a, float b, float c) { return fminf(fminf(a, b), c); }
-__device__ __forceinline__ float vmax3(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
-#endif
 // t0 = max(min(ax, bx), min(ay, by), min(az, bz), tmin), t1 likewise: max and min are associative
 // and commutative on these operands (NaN aside, which the callers exclude or which minNum ignores
 // in any grouping), so the grouping below gives the reference's values.
@@ -708,11 +613,7 @@ __device__ __forceinline__ bool quad_t(const Nodes<kMode>& N, uint32_t off, f3 o
   f3 n = xyz(r0);
   float n_dot = dot(n, d);
   if (fabsf(n_dot) <= 1e-8f) return false;  // |n.d| < 1e-8 (double)
-#if RT2_EXP_FAST_DIV
-  float t = __fdividef(r0.w - dot(n, o), n_dot);
-#else
   float t = (r0.w - dot(n, o)) / n_dot;
-#endif
   if (!(tmin <= t && t <= tmax)) return false;
   float4 r1 = N[off + 1], r2 = N[off + 2], r3 = N[off + 3], r4 = N[off + 4];
   f3 p = o + d * t;
@@ -844,15 +745,9 @@ __device__ __forceinline__ bool quad_cand_u(uint32_t axis, const float* w, f3 o,
     case 1: return quad_cand_aa<0>(w, o, d, t);
     case 2: return quad_cand_aa<1>(w, o, d, t);
     case 3: return quad_cand_aa<2>(w, o, d, t);
-#if RT2_EXP_NO_UNIT_QUAD
-    case 4: return quad_cand_aa<0>(w, o, d, t);
-    case 5: return quad_cand_aa<1>(w, o, d, t);
-    case 6: return quad_cand_aa<2>(w, o, d, t);
-#else
     case 4: return quad_cand_unit<0>(w, o, d, inv, t);
     case 5: return quad_cand_unit<1>(w, o, d, inv, t);
     case 6: return quad_cand_unit<2>(w, o, d, inv, t);
-#endif
     default: return quad_cand_w(w, o, d, t);
   }
 }
@@ -1049,16 +944,6 @@ __device__ __forceinline__ bool trace_stack(const RenderParams& P, const Nodes<k
   uint32_t acc_best = kRefNone;  // accelerated list: record of its current closest child
   while (cur != kRefNone) {
     uint32_t kind = cur >> 28, off = cur & kOffsetMask;
-    if constexpr (RT2_RARE_MIN > 0 && (Has<F, kFeatMedium>() || Has<F, kFeatXform>())) {
-      // Under divergence a branch costs the whole wave whenever one lane takes it: a lane whose
-      // next step is an expensive, infrequent kind (medium, transform entry, accelerated list)
-      // waits until RT2_RARE_MIN lanes are at such steps or no lane has other work, so those
-      // branches run for many lanes at once instead of on almost every trip. Its own step order
-      // is unchanged.
-      const bool rare = kind == kMedium || kind == kXform || kind == kListAcc;
-      const unsigned long long rm = __ballot(rare), cm = __ballot(!rare);
-      if (rare && cm != 0ull && __popcll(rm) < RT2_RARE_MIN) continue;
-    }
     if (kind == kQuad || (Has<F, kFeatSphere>() && kind == kSphere)) {
       float t;
       if (prim_t<F>(N, cur, o, d, time, tmin, tmax, t, cnt)) {
@@ -1186,17 +1071,12 @@ __device__ __forceinline__ bool trace_stack(const RenderParams& P, const Nodes<k
   return any;
 }
 
-// Threaded traversal (small scenes): all lanes of the wave walk the pre-order program P.lin in
-// lockstep. Each lane keeps the index of its next step; the wave executes the smallest pending
-// index, so the step kind is wave-uniform (no divergence between kinds) and the step's program
-// entry and record are scalar loads into SGPRs. A lane whose AABB test misses jumps to the node's
-// skip index. Per lane the visit order is exactly the stack traversal's.
-// the 16 words of step i (entry + first 48 record bytes) for the accelerated-list steps
-#if RT2_WIDE_PROGRAM
-#define RT2_STEP_WORDS(w) const u32x16& w = sw
-#else
-#define RT2_STEP_WORDS(w) const u32x16 w = sld16(P.lin_wide, at * 64u)
-#endif
+// Threaded traversal (small scenes): all lanes of the wave walk the pre-order program in lockstep.
+// Each lane keeps the index of its next step; the wave executes the smallest pending index, so the
+// step kind is wave-uniform (no divergence between kinds) and the step's 64 bytes (program entry +
+// the first 48 bytes of its record, P.lin_wide) are one scalar load into SGPRs. A lane whose AABB
+// test misses jumps to the node's skip index. Per lane the visit order is exactly the stack
+// traversal's.
 // Smallest `next` over the wave's active lanes (one ballot per distinct smaller value).
 __device__ __forceinline__ uint32_t wave_min_next(uint32_t next) {
   uint32_t i = __builtin_amdgcn_readfirstlane(next);
@@ -1209,9 +1089,6 @@ template <uint32_t F, bool kStats, class G>
 __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd, float time, G& path, HitRef& h,
                                              Counters& cnt) {
   const Nodes<kModeLinear> N{reinterpret_cast<const float4*>(P.lind)};  // boundaries / nested xforms
-#if !RT2_WIDE_PROGRAM
-  const void* prog = P.lin;
-#endif
   const void* recs = P.lind;
   f3 o = wo, d = wd;
   const f3 winv = recip3(wd);
@@ -1232,39 +1109,21 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
 #endif
   uint32_t i = wave_min_next(next);  // wave-uniform step = min over live lanes of `next`
   while (i < len) {
-#if RT2_WIDE_PROGRAM
     u32x16 sw = sld16(P.lin_wide, i * 64u);  // entry + the first 48 bytes of its record
-#else
-    u32x16 sw;
-    {
-      const u32x4 e = sld4(prog, i * 16u);
-      sw[0] = e.x, sw[1] = e.y, sw[2] = e.z, sw[3] = e.w;
-      if (e.x == kBvh) {
-        const u32x8 b = sld8(recs, e.z * 16u);
-        for (int j = 0; j < 8; j++) sw[4 + j] = b[j];
-      }
-    }
-#endif
-#define RT2_IS_RUN(k) ((k) == kBvh || (RT2_ACC_RUN && RT2_WIDE_PROGRAM && Has<F, kFeatAccList>() && (k) == kAccBvh))
+#define RT2_IS_RUN(k) ((k) == kBvh || (Has<F, kFeatAccList>() && (k) == kAccBvh))
     if (RT2_IS_RUN(sw[0])) {
-      // A run of BVH steps in a loop of its own: only `next` changes from step to step, so nothing
-      // else is carried (no register copies between kinds) and the step costs the slab test, the
-      // next-index update and the wave-minimum search.
-      const bool allfin = RT2_EXP_NO_FIN_AABB ? false : (bool)__all(fin);
+      // A run of BVH steps (scene BVH and accelerated-list trees) in a loop of their own: only
+      // `next` changes from step to step, so nothing else is carried (no register copies between
+      // kinds) and the step costs the slab test, the next-index update and the wave-minimum search.
+      // A paired step (compile.cpp: word 2 is not i + 1; sphere scenes only) also tests its near
+      // child's box (words 7, 11-15), with the tmax that child's own step would see (nothing runs
+      // between the two in pre-order), and jumps past it.
+      const bool allfin = __all(fin);
       do {
         RT2_WAVE(1);
         RT2_WAVE(2);
-#if RT2_WIDE_PROGRAM && RT2_BVH_SPEC
-        // i + 1 is the wave's next step whenever a lane at i hits the box (pre-order: the near
-        // child follows), so its 64 bytes are fetched now; the load stays in flight (nothing reads
-        // `spec`) until the wait below, which every path out of this iteration passes
-        const uint32_t pi = i + 1u < len ? i + 1u : i;
-        u32x16 spec;
-        asm volatile("s_load_dwordx16 %0, %1, %2" : "=s"(spec) : "s"(P.lin_wide), "s"(pi * 64u));
-#endif
-#if RT2_ACC_RUN && RT2_WIDE_PROGRAM
         if (Has<F, kFeatAccList>() && sw[0] == kAccBvh) {
-          if (next == i) {  // padded slab test of an accelerated list's tree node (as below)
+          if (next == i) {  // padded slab test of an accelerated list's tree node
             if (kStats) cnt.bvh++;
             const float ax = ((uf(sw[4]) - acc_pad) - o.x) * inv.x, bx = ((uf(sw[8]) + acc_pad) - o.x) * inv.x;
             const float ay = ((uf(sw[5]) - acc_pad) - o.y) * inv.y, by = ((uf(sw[9]) + acc_pad) - o.y) * inv.y;
@@ -1273,7 +1132,7 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
             slab_t(ax, bx, ay, by, az, bz, tmin, tmax, t0, t1);
             const bool in = t0 <= t1;
             uint32_t nx = in ? i + 1u : sw[1];
-            if (sw[2] != i + 1u) {  // paired with its near child's step (compile.cpp), same tmax and padding
+            if (sw[2] != i + 1u) {  // paired with its near child's step, same tmax and padding
               const float cx = ((uf(sw[7]) - acc_pad) - o.x) * inv.x, dx = ((uf(sw[13]) + acc_pad) - o.x) * inv.x;
               const float cy = ((uf(sw[11]) - acc_pad) - o.y) * inv.y, dy = ((uf(sw[14]) + acc_pad) - o.y) * inv.y;
               const float cz = ((uf(sw[12]) - acc_pad) - o.z) * inv.z, dz = ((uf(sw[15]) + acc_pad) - o.z) * inv.z;
@@ -1284,30 +1143,11 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
             }
             next = nx;
           }
-        } else
-#endif
-#if RT2_BVH_SELECT && RT2_WIDE_PROGRAM
-        if (allfin) {  // every lane evaluates the slab test; the lanes at step i take its result
-          if (kStats && next == i) cnt.bvh++;
-          const float4 lo = make_float4(uf(sw[4]), uf(sw[5]), uf(sw[6]), 0.0f);
-          const float4 hi = make_float4(uf(sw[8]), uf(sw[9]), uf(sw[10]), 0.0f);
-          const bool in = aabb_hit_fin(lo, hi, o, inv, tmin, tmax);
-          bool in2 = true;
-          if (sw[2] != i + 1u)
-            in2 = aabb_hit_fin(make_float4(uf(sw[7]), uf(sw[11]), uf(sw[12]), 0.0f),
-                               make_float4(uf(sw[13]), uf(sw[14]), uf(sw[15]), 0.0f), o, inv, tmin, tmax);
-          next = next == i ? (in ? (in2 ? sw[2] : sw[3]) : sw[1]) : next;
-        } else
-#endif
-        if (next == i) {
+        } else if (next == i) {
           if (kStats) cnt.bvh++;
           const float4 lo = make_float4(uf(sw[4]), uf(sw[5]), uf(sw[6]), 0.0f);
           const float4 hi = make_float4(uf(sw[8]), uf(sw[9]), uf(sw[10]), 0.0f);
           const bool in = allfin ? aabb_hit_fin(lo, hi, o, inv, tmin, tmax) : aabb_hit(lo, hi, o, inv, tmin, tmax);
-#if RT2_WIDE_PROGRAM
-          // a paired step (compile.cpp: word 2 is not i + 1; sphere scenes only) also tests its near
-          // child's box, with the tmax that child's own step would see (nothing runs between the
-          // two in pre-order)
           uint32_t nx = in ? i + 1u : sw[1];
           if (Has<F, kFeatSphere>() && sw[2] != i + 1u) {
             const float4 lo2 = make_float4(uf(sw[7]), uf(sw[11]), uf(sw[12]), 0.0f);
@@ -1317,7 +1157,6 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
             if (kStats && in) cnt.bvh++;
             nx = in ? (in2 ? sw[2] : sw[3]) : sw[1];
           }
-#endif
 #if RT2_EXP_TWICE & 8
           {
             f3 o2 = o;
@@ -1326,35 +1165,15 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
             asm volatile("" ::"v"((int)in2));
           }
 #endif
-#if RT2_WIDE_PROGRAM
           next = nx;
-#else
-          next = in ? i + 1u : sw[1];
-#endif
         }
         i = wave_min_next(next);
-#if RT2_WIDE_PROGRAM && RT2_BVH_SPEC
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(spec));
-        if (i >= len) break;
-        if (i == pi)
-          sw = spec;
-        else
-          sw = sld16(P.lin_wide, i * 64u);
-#elif RT2_WIDE_PROGRAM
         if (i >= len) break;
         sw = sld16(P.lin_wide, i * 64u);
-#else
-        if (i >= len) break;
-        const u32x4 e = sld4(prog, i * 16u);
-        sw[0] = e.x, sw[1] = e.y, sw[2] = e.z, sw[3] = e.w;
-        if (e.x == kBvh) {
-          const u32x8 b = sld8(recs, e.z * 16u);
-          for (int j = 0; j < 8; j++) sw[4 + j] = b[j];
-        }
-#endif
       } while (RT2_IS_RUN(sw[0]));
       if (i >= len) break;
     }
+#undef RT2_IS_RUN
     const u32x4 st = {sw[0], sw[1], sw[2], sw[3]};
     const uint32_t kind = st.x, off = st.z;
     RT2_WAVE(1);
@@ -1371,27 +1190,15 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
       // order (issue-bound: one candidate at a time beats two interleaved, measured)
       const uint32_t run = st.w;
       uint32_t codes = st.y;
-#if RT2_WIDE_PROGRAM && RT2_QUAD_PREFETCH
-      // the next record of the run is touched (one scalar load into the scalar cache) while this
-      // quad is tested, so its own load later finds the line on chip
-      uint32_t touch = 0;
-#endif
       for (uint32_t k = 0; k < run; k++, codes >>= 3) {
         const uint32_t o0 = off + 5u * k;
         const uint32_t c0 = codes & 7u;
         float t0;
         bool ok0;
         uint32_t kind0;
-#if RT2_WIDE_PROGRAM && RT2_QUAD_PREFETCH
-        if (k + 1u < run) sld_touch(recs, (o0 + 5u) * 16u, touch);
-#endif
         if (c0 >= 4u) {
-#if RT2_WIDE_PROGRAM
           const u32x8 a = k == 0u ? u32x8{sw[4], sw[5], sw[6], sw[7], sw[8], sw[9], sw[10], sw[11]}
                                   : sld8(recs, o0 * 16u);
-#else
-          const u32x8 a = sld8(recs, o0 * 16u);
-#endif
           float ra[8];
 #pragma unroll
           for (int j = 0; j < 8; j++) ra[j] = uf(a[j]);
@@ -1409,9 +1216,6 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
           ok0 = quad_cand_u(c0, w0, o, d, inv, t0);
           kind0 = kQuad;
         }
-#if RT2_WIDE_PROGRAM && RT2_QUAD_PREFETCH
-        sld_wait1(touch);
-#endif
         if (kStats) cnt.quad += 1;
 #if RT2_EXP_TWICE & 16
         {
@@ -1438,14 +1242,10 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
     } else if (Has<F, kFeatSphere>() && kind == kSphere) {
       float t;
       uint32_t ref = make_ref(kind, off);
-#if RT2_WIDE_PROGRAM
       // the sphere record (c0, r | disp, mat) is the step's inline words: no load
       if (kStats) cnt.sphere++;
       const bool hs = sphere_t_rec(make_float4(uf(sw[4]), uf(sw[5]), uf(sw[6]), uf(sw[7])),
                                    make_float4(uf(sw[8]), uf(sw[9]), uf(sw[10]), uf(sw[11])), o, d, time, tmin, tmax, t);
-#else
-      const bool hs = prim_t<F>(N, ref, o, d, time, tmin, tmax, t, cnt);
-#endif
       if (hs) {
         tmax = t;
         prim = ref;
@@ -1477,7 +1277,7 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
         fin = finite3(inv);
       }
     } else if (Has<F, kFeatAccList>() && kind == kListAcc) {
-      RT2_STEP_WORDS(aw);
+      const u32x16& aw = sw;
       // an accelerated HittableList (rt2_layout.h LISTACC): this ray's box padding; its tree's
       // steps follow in pre-order, near child first
       if (kStats) cnt.list++;
@@ -1485,18 +1285,8 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
       const float L = sqrtf(dot(dc, dc)) * 1.0001f + uf(aw[7]);
       acc_pad = (uf(aw[8]) * L + uf(aw[9])) * L + uf(aw[10]);
       acc_best = kRefNone;
-    } else if (Has<F, kFeatAccList>() && kind == kAccBvh) {
-      RT2_STEP_WORDS(aw);
-      if (kStats) cnt.bvh++;
-      // padded slab test as in trace_stack; a miss skips the subtree
-      const float ax = ((uf(aw[4]) - acc_pad) - o.x) * inv.x, bx = ((uf(aw[8]) + acc_pad) - o.x) * inv.x;
-      const float ay = ((uf(aw[5]) - acc_pad) - o.y) * inv.y, by = ((uf(aw[9]) + acc_pad) - o.y) * inv.y;
-      const float az = ((uf(aw[6]) - acc_pad) - o.z) * inv.z, bz = ((uf(aw[10]) + acc_pad) - o.z) * inv.z;
-      float t0, t1;
-      slab_t(ax, bx, ay, by, az, bz, tmin, tmax, t0, t1);
-      if (!(t0 <= t1)) next = st.y;
     } else if (Has<F, kFeatAccList>() && kind == kAccSphere) {
-      RT2_STEP_WORDS(aw);
+      const u32x16& aw = sw;
       // smallest root wins; an equal root goes to the lower child index (aux = the child's
       // record offset in the node array, which is list order)
       if (kStats) cnt.sphere++;
@@ -1512,11 +1302,7 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
     } else if (Has<F, kFeatMedium>() && kind == kMedium) {
       if (kStats) cnt.medium++;
       float t;
-#if RT2_WIDE_PROGRAM
       const u32x4 mr = {sw[4], sw[5], sw[6], sw[7]};  // the medium record, inline
-#else
-      const u32x4 mr = sld4(recs, off * 16u);
-#endif
       if (medium_t_lin<F>(recs, mr, o, d, time, tmin, tmax, path, t, cnt)) {
         tmax = t;
         prim = make_ref(kMedium, off);
@@ -1535,11 +1321,6 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
   return prim != kRefNone;
 }
 
-// Threaded traversal (small scenes): all lanes of the wave walk the pre-order program P.lin in
-// lockstep. Each lane keeps the index of its next step; the wave executes the smallest pending
-// index, so the step kind is wave-uniform (no divergence between kinds) and the step's program
-// entry and record are scalar loads into SGPRs. A lane whose AABB test misses jumps to the node's
-// skip index. Per lane the visit order is exactly the stack traversal's.
 // The closest hit's record in world space (what the reference's rec holds after the chain of
 // TransformedHittable::Hit returns): point, normal, front_face, material.
 template <uint32_t F, int kMode>
@@ -1665,7 +1446,6 @@ __device__ __forceinline__ void camera_ray(const RenderParams& P, G& g, f3& o, f
   } else {
     g.template take<3>(u);  // px, py, time
   }
-#if RT2_KARG_CAMERA
   // pixel00, du, dv, center (words 0-11) and recip_sqrt_spp (word 19) from the argument segment
   constexpr uint32_t kCam = (uint32_t)offsetof(RenderParams, cam);
   static_assert(offsetof(CameraParams, recip_sqrt_spp) == 19 * 4, "CameraParams layout");
@@ -1676,13 +1456,6 @@ __device__ __forceinline__ void camera_ray(const RenderParams& P, G& g, f3& o, f
   f3 du = mk(uf(ca[3]), uf(ca[4]), uf(ca[5]));
   f3 dv = mk(uf(ca[6]), uf(ca[7]), uf(ca[8]));
   f3 c = mk(uf(ca[9]), uf(ca[10]), uf(ca[11]));
-#else
-  const float rs = C.recip_sqrt_spp;
-  f3 p00 = mk(C.pixel00[0], C.pixel00[1], C.pixel00[2]);
-  f3 du = mk(C.du[0], C.du[1], C.du[2]);
-  f3 dv = mk(C.dv[0], C.dv[1], C.dv[2]);
-  f3 c = mk(C.center[0], C.center[1], C.center[2]);
-#endif
   float px = ((float)s_i + u[0]) * rs - 0.5f;
   float py = ((float)s_j + u[1]) * rs - 0.5f;
   f3 pc = (p00 + (((float)x + px) * du)) + (((float)y + py) * dv);
@@ -1750,11 +1523,11 @@ constexpr int MinWaves() {
 // LDS) and stage whole sample octets instead.
 template <uint32_t F, int kMode, bool kStats>
 constexpr bool LdsRng() {
-  return RT2_LDS_RNG && kMode == kModeLinear && !kStats && MinWaves<F, kMode, kStats>() >= 8;
+  return kMode == kModeLinear && !kStats && MinWaves<F, kMode, kStats>() >= 8;
 }
 template <uint32_t F, int kMode, bool kStats>
 constexpr uint32_t StageGroup() {
-  if (!RT2_OCTET_STAGE || kMode != kModeLinear || kStats) return 0u;
+  if (kMode != kModeLinear || kStats) return 0u;
   // octets need 5.25 KB per wave: with the LDS Philox blocks beside them they fit no occupancy >= 7
   return MinWaves<F, kMode, kStats>() <= 7 && !LdsRng<F, kMode, kStats>() ? 8u : 4u;
 }
@@ -1791,9 +1564,6 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
     __shared__ uint32_t s_rng[(kBlock / 64) * 4 * 64];
     path.rbw = s_rng + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * 256u;
   }
-  path.k0 = P.seed_lo;
-  path.k1 = P.seed_hi;
-  path.width = (uint32_t)P.width;
   path.xy = 0;
   path.start(0);
   path.r0 = path.r1 = path.r2 = path.r3 = 0;
@@ -1832,7 +1602,7 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
     // items still spread over all waves.
     unsigned long long mask = __ballot(need && !idle);
     if (mask != 0ull) {
-      const LoopArgs A = RT2_LOOP_ARGS();
+      const LoopArgs A = loop_args();
       const uint32_t max_depth = (uint32_t)A.max_depth();  // <= 0xFFFF (rt2_tracer_set_max_depth)
       const uint32_t count = (uint32_t)__popcll(mask);
       const uint32_t avail = bend - bnext;
@@ -1968,7 +1738,7 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
         } else {
           resolve_hit<F>(N, h, ro, rd, rtime, hp, hn, front, mat);
         }
-        const ShadeArgs S = RT2_SHADE_ARGS();
+        const ShadeArgs S = shade_args();
         float4 m0 = S.materials[2 * mat], m1 = S.materials[2 * mat + 1];
         uint32_t type = bits(m0.x);
         if (type == kMatDiffuseLight) {
@@ -2025,7 +1795,7 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
     RT2_STAMP(st_shade);
     if (done) {
       // this frame's sample, summed in frame order by accumulate_kernel (RayTracer.cpp:64)
-      const LoopArgs A = RT2_LOOP_ARGS();
+      const LoopArgs A = loop_args();
       const uint32_t lidx = local_index(A, path.xy);
       const uint32_t fr = path.frame - (uint32_t)A.frame_begin();  // launch-relative frame
       const uint32_t slot = fr & (kOctet - 1u);

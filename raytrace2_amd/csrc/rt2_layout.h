@@ -40,6 +40,25 @@ constexpr uint32_t kRefNone = 0xFFFFFFFFu;
 // rotates from period to period, so no rank is tied to one phase of a periodic cost pattern. A rank
 // stores its rows compactly in increasing y: local row l = p * band_h + (y % band_h).
 inline constexpr int BandRank(int band, int world) { return (band % world + band / world) % world; }
+// Rows of the largest rank's band stack: every rank's accumulation is allocated this tall and the
+// gather sends this many rows from each rank (padding rows zero), so the root receives rank-major
+// stacks [world][BandRowsMax][W]. band_h 0 = one band of the whole height.
+inline constexpr int BandRowsMax(int height, int band_h, int world) {
+  if (height <= 0) return 0;
+  const int bh = band_h > 0 ? band_h : height;
+  const int bands = (height + bh - 1) / bh;
+  return (bands + world - 1) / world * bh;
+}
+// Where image row y lives in the gathered stacks: the owning rank and its rank-local row (the
+// de-interleave map of gather.hip and of rt2_deinterleave_host; constexpr, so host and device).
+struct BandRow {
+  int rank, row;
+};
+inline constexpr BandRow BandSource(int y, int band_h, int world) {
+  if (band_h <= 0) return BandRow{0, y};  // one band: rank 0 holds every row
+  const int band = y / band_h, period = band / world;
+  return BandRow{BandRank(band, world), period * band_h + (y - band * band_h)};
+}
 constexpr uint32_t kOffsetMask = 0x0FFFFFFFu;
 inline constexpr uint32_t make_ref(uint32_t kind, uint32_t off) { return (kind << 28) | off; }
 

@@ -10,20 +10,35 @@ from __future__ import annotations
 
 from typing import List, Optional
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
-from .tracer import local_rows
+from ._native import check, lib
+from .tracer import _fp, local_rows
 
 
 def band_rows_max(height: int, band_h: int, world: int) -> int:
-    """Upper bound of the rows a rank owns (send-buffer height, equal on every rank)."""
-    bands = -(-height // band_h)
-    return -(-bands // world) * band_h
+    """Rows every rank sends (its band stack padded to the largest rank's; rt2_band_rows_max, the
+    same function the C ABI's gather uses)."""
+    return check(lib.rt2_band_rows_max(int(height), int(band_h), int(world)))
+
+
+def deinterleave(stacks: np.ndarray, height: int, band_h: int) -> np.ndarray:
+    """Rank-major padded band stacks (world, max_rows, W, C) -> the image (H, W, C), through the C
+    ABI's host de-interleave (rt2_layout.h BandSource, the map of the root's GPU kernel)."""
+    stacks = np.ascontiguousarray(stacks, np.float32)
+    world, max_rows, w, c = stacks.shape
+    out = np.empty((height, w, c), np.float32)
+    check(lib.rt2_deinterleave_host(_fp(stacks), _fp(out), w, height, int(band_h), world, max_rows, c))
+    return out
 
 
 class BandGather:
-    """Gathers (rows_r, W, C) float32 band stacks of every rank into one (H, W, C) image on rank 0."""
+    """Gathers (rows_r, W, C) float32 band stacks of every rank into one (H, W, C) image on rank 0:
+    every rank sends its padded stack (band_rows_max rows) with one torch.distributed gather into a
+    rank-major buffer, which rank 0 de-interleaves with the C ABI's layout code (the buffer ncclGather
+    fills inside rt2_tracer_gather has the same layout)."""
 
     def __init__(self, height: int, width: int, band_h: int, world: int, rank: int, device: torch.device,
                  channels: int = 3, group: Optional[dist.ProcessGroup] = None):
@@ -32,29 +47,25 @@ class BandGather:
         self.rows = [local_rows(height, band_h, r, world) for r in range(world)]
         self.max_rows = band_rows_max(height, band_h, world)
         self.send = torch.zeros((self.max_rows, width, channels), dtype=torch.float32, device=device)
-        self.recv: Optional[List[torch.Tensor]] = None
+        self.stacks: Optional[torch.Tensor] = None
         self.image: Optional[torch.Tensor] = None
-        self.index: Optional[List[torch.Tensor]] = None
         if rank == 0:
-            self.recv = [torch.zeros_like(self.send) for _ in range(world)]
-            self.image = torch.zeros((height, width, channels), dtype=torch.float32, device=device)
-            self.index = [torch.tensor(r, dtype=torch.long, device=device) for r in self.rows]
+            self.stacks = torch.zeros((world, self.max_rows, width, channels), dtype=torch.float32, device=device)
+            self.image = torch.zeros((height, width, channels), dtype=torch.float32)
 
     def local_view(self) -> torch.Tensor:
         """The part of the send buffer this rank fills (its local rows)."""
         return self.send[:len(self.rows[self.rank])]
 
     def gather(self) -> Optional[torch.Tensor]:
-        """Collective: every rank calls it; rank 0 returns the assembled image, others None."""
+        """Collective: every rank calls it; rank 0 returns the assembled image (host), others None."""
         if self.world == 1:
-            n = len(self.rows[0])
-            self.image[:n].copy_(self.send[:n])  # rows == all rows, already in order
-            return self.image
-        dist.gather(self.send, self.recv if self.rank == 0 else None, dst=0, group=self.group)
-        if self.rank != 0:
-            return None
-        for r in range(self.world):
-            n = len(self.rows[r])
-            if n:
-                self.image.index_copy_(0, self.index[r], self.recv[r][:n])
+            self.stacks[0].copy_(self.send)
+        else:
+            recv: Optional[List[torch.Tensor]] = list(self.stacks.unbind(0)) if self.rank == 0 else None
+            dist.gather(self.send, recv, dst=0, group=self.group)
+            if self.rank != 0:
+                return None
+        img = deinterleave(self.stacks.cpu().numpy(), self.height, self.band_h)
+        self.image.copy_(torch.from_numpy(img))
         return self.image

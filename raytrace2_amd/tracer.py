@@ -349,6 +349,14 @@ class RayTracer:
         """Launch the queued Update()/Render() frames now (does not wait for them)."""
         check(lib.rt2_tracer_flush(self._h))
 
+    def query(self) -> int:
+        """1 when every GPU has finished the work enqueued so far, 0 while some is still running
+        (launches queued frames first, like flush(); never waits)."""
+        r = lib.rt2_tracer_query(self._h)
+        if r < 0:
+            check(r)
+        return r
+
     def set_lazy_frames(self, max_queued: int) -> None:
         check(lib.rt2_tracer_set_lazy_frames(self._h, int(max_queued)))
 

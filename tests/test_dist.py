@@ -1,7 +1,10 @@
-"""N>1 path on the CPU: world_size-2 gloo process group running the same band partition + gather
-(raytrace2_amd.dist.BandGather) the bench uses over RCCL. Each rank renders its row bands with the
-CPU restatement (stand-in renderer, no GPU here); the gathered image must equal the single-process
-render bit for bit, because sample streams are keyed by global pixel and frame."""
+"""N>1 path on the CPU: world_size-2/3 gloo process groups running the band partition + gather of the
+C ABI's multi-GPU path: every rank sends its band stack padded to rt2_band_rows_max rows, the root
+receives the rank-major stacks (the layout ncclGather delivers inside rt2_tracer_gather) and
+de-interleaves them with rt2_deinterleave_host, the same index map (rt2_layout.h BandSource) as the
+root's GPU kernel. Each rank renders its row bands with the CPU restatement (stand-in renderer, no GPU
+here); the gathered image must equal the single-process render bit for bit, because sample streams
+are keyed by global pixel and frame."""
 import os
 import socket
 
@@ -68,3 +71,23 @@ def test_band_partition_covers_every_row_once(h, band_h, world):
         owners = [band_rank(p * world + q, world) for q in range(world)]
         assert sorted(owners) == list(range(world))
         assert owners[0] == p % world
+
+
+@pytest.mark.parametrize("h,band_h,world", [(45, 8, 3), (47, 16, 1), (40, 16, 1), (10, 8, 4), (33, 2, 8), (9, 0, 1),
+                                            (1024, 2, 8), (7, 1, 7)])
+def test_c_abi_deinterleave_inverts_the_partition(h, band_h, world):
+    """rt2_band_rows_max / rt2_deinterleave_host (the C ABI's gather layout) against the Python
+    statement of the partition: random band stacks, padded rows poisoned, reassemble exactly."""
+    from raytrace2_amd.dist import band_rows_max, deinterleave
+    from raytrace2_amd.tracer import assemble_bands, local_rows
+    w = 5
+    rng = np.random.default_rng(h * 31 + band_h + world)
+    mr = band_rows_max(h, band_h, world)
+    rows = [local_rows(h, band_h, r, world) for r in range(world)]
+    assert mr == max(len(r) for r in rows) or (band_h and mr - max(len(r) for r in rows) < band_h)
+    parts = [rng.standard_normal((len(r), w, 3)).astype(np.float32) for r in rows]
+    stacks = np.full((world, mr, w, 3), np.nan, np.float32)  # padding must never be read
+    for r, p in enumerate(parts):
+        stacks[r, :len(p)] = p
+    img = deinterleave(stacks, h, band_h)
+    assert np.array_equal(img.view(np.uint32), assemble_bands(parts, h, band_h).view(np.uint32))

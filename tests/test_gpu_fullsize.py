@@ -35,17 +35,20 @@ def _check(name, w, h, spp, frames, **kw):
     return acc, rc
 
 
-def _check_continuation(name, w, h, spp, k, n, **part):
-    """GPU frames 0..n vs oracle frames k..n started from the GPU's accumulation at frame k."""
+def _check_continuation(name, w, h, spp, k, n, launch=None, **part):
+    """GPU frames 0..n vs oracle frames k..n started from the GPU's accumulation at frame k.
+    `launch`: GPU launch-shape settings (launch_frames / sample_budget) for both GPU renders."""
     from oracle.oracle import OracleScene
-    a_k, rc_k, _, _ = gpu_render(name, w, h, spp, k, **part)
-    a_n, rc_n, _, _ = gpu_render(name, w, h, spp, n, **part)
+    launch = launch or {}
+    a_k, rc_k, _, _ = gpu_render(name, w, h, spp, k, **part, **launch)
+    a_n, rc_n, st_n, _ = gpu_render(name, w, h, spp, n, **part, **launch)
     o = OracleScene(scene_path(name), SEED)
     o_acc = a_k.copy()
     o_rc = np.zeros_like(rc_k)
     o.render(w, h, spp, n - k, frame_begin=k, accum=o_acc, ray_counts=o_rc, forward=True, threads=THREADS, **part)
     np.testing.assert_array_equal(rc_n - rc_k, o_rc)
     assert _same(a_n, o_acc)
+    return st_n
 
 
 def test_c1_cornell_400_at_64spp_full_image():
@@ -122,3 +125,34 @@ def test_frame_tiles_off_on_book2(monkeypatch):
     """Book 2 with frame tiles switched off (pixel tiles, 64-frame chunks) against the oracle."""
     monkeypatch.setenv("RT2_FRAME_TILES", "0")
     _check("book2_final_scene_10000_samples", 800, 800, 10000, 12, band_h=8, rank=50, world=100)
+
+
+def _band_frame_bytes(w, h, band_h, rank, world):
+    rows = sum(1 for y in range(h) if ((y // band_h) % world + (y // band_h) // world) % world == rank)
+    return w * rows * 12
+
+
+@pytest.mark.parametrize("boundary,how", [(2000, "launch_frames"), (2232, "sample_budget")])
+def test_c5_book2_across_a_launch_boundary(boundary, how):
+    """Book 2 (C5: 800x800 @ 10000 spp, frame tiles) across a launch boundary: the bench's 16 GiB
+    sample budget cuts its render into launches of 2232 frames (budget_frames rounded to octets);
+    frames boundary-10 .. boundary+10 on a full-width band are continued by the oracle from the GPU's
+    accumulation and must match bit for bit (RayTracer.cpp:55-70 renders every frame alike)."""
+    part = dict(band_h=8, rank=50, world=100)
+    launch = ({"launch_frames": boundary} if how == "launch_frames" else
+              {"sample_budget": boundary * _band_frame_bytes(800, 800, **part)})
+    st = _check_continuation("book2_final_scene_10000_samples", 800, 800, 10000, boundary - 10, boundary + 10,
+                             launch=launch, **part)
+    assert st["launches"] == 2
+
+
+@pytest.mark.parametrize("boundary,how", [(1333, "launch_frames"), (1360, "sample_budget")])
+def test_c4_cornell_volume_across_a_launch_boundary(boundary, how):
+    """Cornell volume (C4: 1024^2 @ 4000 spp) across the bench's launch boundary (16 GiB budget:
+    launches of 1360 frames) and an odd one (1333, launch_frames), continued by the oracle."""
+    part = dict(band_h=8, rank=40, world=128)
+    launch = ({"launch_frames": boundary} if how == "launch_frames" else
+              {"sample_budget": boundary * _band_frame_bytes(1024, 1024, **part)})
+    st = _check_continuation("cornell_box_volume", 1024, 1024, 4000, boundary - 10, boundary + 10, launch=launch,
+                             **part)
+    assert st["launches"] == 2

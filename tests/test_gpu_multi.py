@@ -114,10 +114,12 @@ def test_multi_reset_resize_and_explicit_gather():
     tr.close()
 
 
-def test_join_world_one():
-    """The one-process-per-GPU path (rt2_comm_unique_id + rt2_tracer_join = ncclCommInitRank)."""
+@pytest.mark.parametrize("h", [40, 47])
+def test_join_world_one(h):
+    """The one-process-per-GPU path (rt2_comm_unique_id + rt2_tracer_join = ncclCommInitRank); band
+    height 16 does not divide the image height, so the gather sends padding rows (allocated, zero)."""
     import raytrace2_amd as R
-    w, h, spp, frames = 48, 40, 16, 4
+    w, spp, frames = 48, 16, 4
     acc, px, _, _ = _plain("cornell_box_original", w, h, spp, frames, counts=False)
     sc = R.Scene(scene_path("cornell_box_original"), SEED)
     tr = R.RayTracer(sc, 0)
@@ -200,3 +202,37 @@ def test_partitions_with_frame_tiles(monkeypatch):
     macc, mpx, mrc, mst, _ = _multi("cornell_box_original", w, h, spp, frames, devices=[0] * 3, band_h=2)
     assert _same(macc, acc) and np.array_equal(mpx, px) and np.array_equal(mrc, rc)
     assert mst["rays"] == st["rays"]
+
+
+def test_multi_launch_render_does_not_block_the_host():
+    """A render of several launches per GPU (sample-buffer budget) is enqueued without the host
+    waiting for any of them: chunk tables go up stream-ordered from pinned staging, so the
+    one-process tracer keeps every GPU busy (RayTracer.cpp:69 keeps every worker busy). Two
+    partitions on one GPU stand in for two GPUs; the result is bit-identical to one plain render."""
+    import time
+    import raytrace2_amd as R
+    w, h, spp, frames = 256, 256, 1000, 600
+    acc, px, _, st = _plain("cornell_box_original", w, h, spp, frames, counts=False)
+    sc = R.Scene(scene_path("cornell_box_original"), SEED)
+    tr = R.RayTracer(sc, devices=[0, 0], band_h=2)
+    tr.set_seed(SEED)
+    tr.SetSamplesPerPixel(spp)
+    tr.OnResize((w, h))
+    tr.set_sample_budget(200 * w * (h // 2) * 12)  # 200 frames per launch: 3 launches per part
+    tr.Render(7)  # warm: kernels loaded, buffers sized (another chunk schedule than the timed render)
+    tr.synchronize()
+    tr.Reset()
+    tr.reset_stats()
+    tr.Render(frames)
+    t0 = time.perf_counter()
+    tr.flush()
+    host_s = time.perf_counter() - t0
+    busy = tr.query()
+    tr.synchronize()
+    mst = tr.stats()
+    assert mst["launches"] == 3, mst["launches"]
+    assert busy == 0, "the GPU was idle right after flush(): the host waited for the launches"
+    assert host_s * 1e3 < 0.5 * mst["kernel_ms"], (host_s * 1e3, mst["kernel_ms"])
+    assert _same(tr.Accumulation(), acc) and np.array_equal(tr.Pixels(), px)
+    assert mst["rays"] == st["rays"]
+    tr.close()

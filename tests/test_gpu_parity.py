@@ -71,7 +71,7 @@ def test_update_equals_render_and_chunking(have_gpu):
     assert s4["launches"] == 7 and s5["launches"] == 4
 
 
-@pytest.mark.parametrize("name", ["cornell_box_original", "final_render_book_1"])
+@pytest.mark.parametrize("name", ["cornell_box_original", "final_render_book_1", "book2_final_scene_10000_samples"])
 def test_work_split_is_invisible(have_gpu, name):
     # A pixel's frames cut into chunks rendered by different lanes (any chunk size, any wave batch,
     # several launches when the sample buffer is small) must sum to the same bits: samples are
