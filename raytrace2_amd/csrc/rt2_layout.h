@@ -170,7 +170,10 @@ struct CameraParams {
 
 struct StatsCounters {  // u64 slots written by the kernel
   enum { kRays = 0, kBvhTests, kQuadTests, kSphereTests, kXformVisits, kMediumTests, kListVisits, kPaths, kCount };
-  enum { kOverflow = kCount, kStamps = 9, kDiag = 16, kSlots = 32 };  // stamps / diag: diagnostic builds
+  // stamps / diag: diagnostic builds; tail compaction: paths moved, taken in the launch, taken by
+  // the drain launch, take attempts, attempts that saw published paths
+  enum { kOverflow = kCount, kStamps = 9, kMigrated = 13, kResumed = 14, kResumedDrain = 15, kDiag = 16,
+         kTakeTries = 24, kTakeSeen = 25, kSlots = 32 };
 };
 constexpr int kStatsSlots = StatsCounters::kSlots;
 
@@ -238,6 +241,16 @@ struct RenderParams {
   uint32_t frame_tiles;
   uint32_t frame_tile;
   Magic div_frame_tile, div_width;
+  // Launch-tail compaction (the item queue is empty; RayTracer.cpp:69's work stealing keeps every
+  // worker busy to the end, this keeps every lane busy): a wave with at most tail_min paths left
+  // moves them to the migrant queue and exits; waves with free lanes take queued paths; a drain
+  // launch (drain = 1: no items, no moves) finishes what is left. An entry is kMigrantWords 8-byte
+  // granules {epoch << 32 | word} (self-validating: written and read with no other ordering);
+  // work_counter[1] = entries reserved, work_counter[2] = entries taken. tail_min 0: off.
+  unsigned long long* migrants;
+  uint32_t mcap, epoch, tail_min, drain;
 };
+constexpr uint32_t kMigrantWords = 16;  // ray origin, direction, throughput, time, depth/frames, frame,
+                                        // pixel, stratum, RNG draw count, the item's rays
 
 }  // namespace rt2
