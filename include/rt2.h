@@ -123,13 +123,6 @@ RT2_API int rt2_tracer_set_sample_budget(rt2_tracer* tr, uint64_t bytes);
 /* Most work items a GPU wave reserves with one atomic (default 64); batches shrink as the launch
  * drains. */
 RT2_API int rt2_tracer_set_batch_max(rt2_tracer* tr, int items);
-/* Launch-tail compaction: once a launch has handed out its last work item, a GPU wave left with at
- * most `min_paths` (0..64; default 16, RT2_TAIL_MIN) paths moves them to a queue in device memory
- * and exits, and waves with free lanes take queued paths, so the last paths of a launch run in
- * full waves instead of in waves of a few lanes each; a second, short launch finishes the paths
- * still queued at the end. A path computes the same values on any lane (its random stream is keyed
- * by pixel and frame), so results are unchanged. 0 = off. */
-RT2_API int rt2_tracer_set_tail_compaction(rt2_tracer* tr, int min_paths);
 /* Launch shape of the last render: persistent workgroups, frames of its first chunk, kernel variant. */
 RT2_API int rt2_tracer_last_launch(const rt2_tracer* tr, int* grid, int* chunk_frames, int* variant);
 RT2_API int rt2_tracer_on_resize(rt2_tracer* tr, int width, int height);
@@ -228,9 +221,6 @@ typedef struct {
    * and kernel_ms (the largest per-GPU sum). */
   uint64_t gathers;
   double gather_ms;
-  /* launch-tail compaction: paths moved to the migrant queue by waves that ran low on work, and
-   * paths taken from it (equal after every launch: none is lost) */
-  uint64_t migrated, resumed;
 } rt2_stats;
 RT2_API int rt2_tracer_get_stats(rt2_tracer* tr, rt2_stats* out);
 RT2_API int rt2_tracer_reset_stats(rt2_tracer* tr);

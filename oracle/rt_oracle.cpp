@@ -16,8 +16,9 @@
 //  * RandReal(): Philox4x32-10 counter stream keyed by (seed, pixel, frame) instead of the
 //    thread_local std::minstd_rand seeded from std::random_device (Math.hpp:9-13).
 //  * Perlin tables are drawn from a Philox stream keyed by (seed, noise texture ordinal).
-//  * log() in ConstantMedium and sin() in the marble texture are evaluated in double and
-//    rounded once (the reference calls glibc logf/sinf; difference <= 1 ulp).
+//  * log() in ConstantMedium is the shared float polynomial LogU (within 1 ulp; the reference calls
+//    glibc logf, itself within an ulp); sin() in the marble texture is evaluated in double and
+//    rounded once (the reference calls sinf; difference <= 1 ulp).
 //  * pow(1-cos, 5) in Schlick is an explicit double multiplication chain (reference: std::pow).
 //  * RandUnitVec3 / RandInUnitDisk draw their (identical) distributions by inverse-CDF maps
 //    instead of rejection loops, with a shared polynomial sin/cos (see CosSin2Pi).
@@ -263,6 +264,39 @@ inline void CosSin2Pi(float v, float& c, float& s) {
     default: c = sp; s = -cp; break;
   }
 }
+// ln(u) of a 24-bit uniform u in [0, 1) (ConstantMedium.cpp:38 takes std::log(RandReal())): -inf
+// at 0, else e ln2 + log1p(f) with u = 2^e (1 + f), 1 + f in [sqrt(1/2), sqrt(2)), log1p by a
+// degree-10 polynomial f + f^2 Q(f) (Q of degree 8, max 0.7 ulp over the range) and ln2 split so
+// that e ln2_hi is exact; within 1 ulp of ln(u) for every u (tests/test_oracle_kat.py). Float
+// operations in a fixed order, fused multiply-adds explicit: the kernel (render.hip log_u) computes
+// the same bits. (The reference's glibc logf is itself not correctly rounded; both are within an ulp.)
+inline float LogU(float u) {
+  if (u == 0.0f) return -INFINITY;
+  uint32_t b;
+  memcpy(&b, &u, 4);
+  int e = (int)(b >> 23) - 127;
+  const uint32_t mb = (b & 0x007FFFFFu) | 0x3F800000u;
+  float m;
+  memcpy(&m, &mb, 4);
+  if (m > 1.41421354f) {
+    m = m * 0.5f;
+    e += 1;
+  }
+  const float f = m - 1.0f;
+  float q = -0.07477458566427231f;
+  q = std::fma(q, f, 0.12822002172470093f);
+  q = std::fma(q, f, -0.13261467218399048f);
+  q = std::fma(q, f, 0.1419624537229538f);
+  q = std::fma(q, f, -0.16608606278896332f);
+  q = std::fma(q, f, 0.2000119835138321f);
+  q = std::fma(q, f, -0.2500157654285431f);
+  q = std::fma(q, f, 0.3333333730697632f);
+  q = std::fma(q, f, -0.49999988079071045f);
+  const float l1p = std::fma(f * f, q, f);
+  const float ef = (float)e;
+  return std::fma(ef, 0.693145751953125f, std::fma(ef, 1.42860677e-06f, l1p));
+}
+
 // Math.hpp:26-43 draw RandUnitVec3 = normalize(RandInUnitSphere()) by rejection in [-1,1]^3 and
 // RandInUnitDisk by rejection in [-1,1]^2. The same distributions (uniform on the unit sphere /
 // in the unit disk) are drawn here by the inverse-CDF maps, two uniforms each and no retry loop
@@ -578,7 +612,7 @@ struct ConstantMedium : Hittable {
     rec1.t = (float)std::fmax((double)rec1.t, 0.0);
     float ray_len = length(r.direction);
     float dist_inside = (rec2.t - rec1.t) * ray_len;
-    float hit_dist = neg_inv_density * (float)std::log((double)c.rng->RandReal());
+    float hit_dist = neg_inv_density * LogU(c.rng->RandReal());
     if (hit_dist > dist_inside) return false;
     rec.t = rec1.t + hit_dist / ray_len;
     rec.point = r.At(rec.t);
@@ -1440,12 +1474,17 @@ void oracle_uniforms(uint64_t seed, uint32_t pixel, uint32_t frame, int n, float
 }
 
 // n draws of RandUnitVec3 (which = 0) or RandInUnitDisk (which = 1) from the path stream of
-// (seed, pixel, frame), 3 floats each; which = 2: CosSin2Pi of the n uniforms in `in` (2 floats each)
+// (seed, pixel, frame), 3 floats each; which = 2: CosSin2Pi of the n uniforms in `in` (2 floats each);
+// which = 3: LogU of the n values in `in` (1 float each)
 void oracle_samples(int which, uint64_t seed, uint32_t pixel, uint32_t frame, int n, const float* in, float* out) {
   Rng g(seed, pixel, frame, kTagPath);
   for (int i = 0; i < n; i++) {
     if (which == 2) {
       CosSin2Pi(in[i], out[2 * i], out[2 * i + 1]);
+      continue;
+    }
+    if (which == 3) {
+      out[i] = LogU(in[i]);
       continue;
     }
     vec3 v = which == 0 ? RandUnitVec3(g) : RandInUnitDisk(g);

@@ -54,9 +54,7 @@ class Stats(ctypes.Structure):
                                                                            ("stamps", ctypes.c_uint64 * 4),
                                                                            ("diag", ctypes.c_uint64 * 8),
                                                                            ("gathers", ctypes.c_uint64),
-                                                                           ("gather_ms", ctypes.c_double),
-                                                                           ("migrated", ctypes.c_uint64),
-                                                                           ("resumed", ctypes.c_uint64)]
+                                                                           ("gather_ms", ctypes.c_double)]
 
     def as_dict(self):
         d = {n: (getattr(self, n) if n in ("kernel_ms", "gather_ms") else int(getattr(self, n))) for n, _ in self._fields_
@@ -116,7 +114,6 @@ def _load():
         "rt2_tracer_set_work_split": (i32, [vp, i32]),
         "rt2_tracer_set_sample_budget": (i32, [vp, u64]),
         "rt2_tracer_set_batch_max": (i32, [vp, i32]),
-        "rt2_tracer_set_tail_compaction": (i32, [vp, i32]),
         "rt2_tracer_pixels_async": (i32, [vp, ctypes.POINTER(ctypes.c_uint8)]),
         "rt2_tracer_query": (i32, [vp]),
         "rt2_host_alloc": (i32, [ctypes.c_size_t, ctypes.POINTER(vp)]),

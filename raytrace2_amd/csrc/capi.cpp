@@ -108,17 +108,6 @@ struct rt2_tracer {
   };
   std::vector<Staging> staging;
   int batch_max = 64;                      // most work items a wave reserves with one atomic
-  // launch-tail compaction (RenderParams::migrants): a wave with at most tail_min paths left after
-  // the item queue is empty moves them to other waves (0: off, no drain launch)
-  int tail_min = 16;
-  unsigned long long* d_migrants = nullptr;
-  uint32_t migrant_cap = 0;
-  uint32_t epoch = 0;  // per launch, never 0 (entries of earlier launches never match)
-#if (defined(RT2_EXP_ENDTIME) && RT2_EXP_ENDTIME) || (defined(RT2_EXP_WAVESTEPS) && RT2_EXP_WAVESTEPS)
-  bool diag_build = true;  // a diagnostic build: its kernel fills the diag slots
-#else
-  bool diag_build = false;
-#endif
   int last_chunk_frames = 0;
   int occ_key = -1, occ_blocks = 1;  // cached occupancy of the last kernel instantiation
   size_t occ_lds = 0;
@@ -538,7 +527,6 @@ int rt2_tracer_create(const rt2_scene* s, int device, rt2_tracer** out) {
   if (const char* e = getenv("RT2_CHUNK_ALIGN")) t->chunk_align = e[0] != '0';
   if (const char* e = getenv("RT2_FRAME_TILES")) t->frame_tiles_env = e[0] == '1' ? 1 : 0;
   if (const char* e = getenv("RT2_FRAME_TILE_LEN")) t->frame_tile_len = std::max(1, std::min(atoi(e), 64));
-  if (const char* e = getenv("RT2_TAIL_MIN")) t->tail_min = std::max(0, std::min(atoi(e), 64));
   // App.cpp:122-125,157: scene dims when present, else the window default 1600x900
   int w = s->scene.dims_x > 0 && s->scene.dims_y > 0 ? s->scene.dims_x : 1600;
   int h = s->scene.dims_x > 0 && s->scene.dims_y > 0 ? s->scene.dims_y : 900;
@@ -583,7 +571,6 @@ void rt2_tracer_destroy(rt2_tracer* t) {
   (void)hipFree(t->d_lind);
   (void)hipFree(t->d_work);
   (void)hipFree(t->d_stats);
-  if (t->d_migrants) (void)hipFreeAsync(t->d_migrants, t->stream);
   if (t->d_chunks) (void)hipFreeAsync(t->d_chunks, t->stream);
   if (t->stream) (void)hipStreamSynchronize(t->stream);
   for (auto& st : t->staging) {
@@ -693,13 +680,6 @@ int rt2_tracer_set_batch_max(rt2_tracer* t, int items) {
   if (!t || items < 1) return Fail(RT2_ERR_INVALID, "batch must be >= 1");
   RT2_FORWARD(t, rt2_tracer_set_batch_max(p, items));
   t->batch_max = items;
-  return RT2_OK;
-}
-
-int rt2_tracer_set_tail_compaction(rt2_tracer* t, int min_paths) {
-  if (!t || min_paths < 0 || min_paths > 64) return Fail(RT2_ERR_INVALID, "min_paths must be in [0, 64]");
-  RT2_FORWARD(t, rt2_tracer_set_tail_compaction(p, min_paths));
-  t->tail_min = min_paths;
   return RT2_OK;
 }
 
@@ -1037,21 +1017,6 @@ int LaunchFrames(rt2_tracer* t, int n_frames) {
   }
   int rc = UploadChunks(t, tabs);
   if (rc != RT2_OK) return rc;
-  // migrant queue: room for every resident lane's path twice over (a path can move more than once);
-  // when it is full, waves keep their paths (slower tail, same results)
-  const bool tail = t->tail_min > 0;
-  if (tail && (uint64_t)t->migrant_cap < 2ull * (uint64_t)resident) {
-    if (t->d_migrants) HIP_TRY(hipFreeAsync(t->d_migrants, t->stream));
-    t->d_migrants = nullptr;
-    t->migrant_cap = 0;
-    const size_t cap = 2 * (size_t)resident;
-    HIP_TRY(hipMallocAsync((void**)&t->d_migrants, cap * kMigrantWords * 8, t->stream));
-    HIP_TRY(hipMemsetAsync(t->d_migrants, 0, cap * kMigrantWords * 8, t->stream));  // epoch 0: never valid
-    t->migrant_cap = (uint32_t)cap;
-  }
-  p.migrants = t->d_migrants;
-  p.mcap = t->migrant_cap;
-  p.tail_min = tail ? (uint32_t)t->tail_min : 0u;
   for (const Launch& L : launches) {
     p.frame_begin = L.frame_begin;
     p.n_frames = L.n_frames;
@@ -1072,19 +1037,10 @@ int LaunchFrames(rt2_tracer* t, int n_frames) {
     grid = std::max(grid, 1);
     t->last_grid = grid;
     t->last_chunk_frames = L.first_len;
-    HIP_TRY(hipMemsetAsync(t->d_work, 0, 4 * sizeof(uint32_t), t->stream));  // items, migrants reserved / taken
-    if (++t->epoch == 0) t->epoch = 1;
-    p.epoch = t->epoch;
-    p.drain = 0;
+    HIP_TRY(hipMemsetAsync(t->d_work, 0, sizeof(uint32_t), t->stream));
     hipEvent_t e0 = TakeEvent(t), e1 = TakeEvent(t);
     if (e0) HIP_TRY(hipEventRecord(e0, t->stream));
     HIP_TRY(LaunchRender(p, variant, counting, grid, t->stream));
-    if (tail) {  // the paths still queued when the last wave of the launch left
-      RenderParams d = p;
-      d.drain = 1;
-      d.n_items = 0;
-      HIP_TRY(LaunchRender(d, variant, counting, grid, t->stream));
-    }
     if (e1) HIP_TRY(hipEventRecord(e1, t->stream));
     if (e0 && e1) t->pending.emplace_back(e0, e1);
     HIP_TRY(LaunchAccumulate(t->d_samples, t->d_accum, t->d_pixels, p.local_pixels, p.n_frames,
@@ -1463,8 +1419,6 @@ int rt2_tracer_get_stats(rt2_tracer* t, rt2_stats* o) {
       for (int k = 0; k < 8; k++) sum.diag[k] += s.diag[k];
       sum.gathers += s.gathers;
       sum.gather_ms += s.gather_ms;
-      sum.migrated += s.migrated;
-      sum.resumed += s.resumed;
     }
     *o = sum;
     return RT2_OK;
@@ -1483,15 +1437,8 @@ int rt2_tracer_get_stats(rt2_tracer* t, rt2_stats* o) {
   o->medium_tests = s[StatsCounters::kMediumTests];
   o->list_visits = s[StatsCounters::kListVisits];
   o->overflow = s[StatsCounters::kCount];
-  o->migrated = s[StatsCounters::kMigrated];
-  o->resumed = s[StatsCounters::kResumed] + s[StatsCounters::kResumedDrain];
   for (int k = 0; k < 4; k++) o->stamps[k] = s[StatsCounters::kStamps + k];
   for (int k = 0; k < 8; k++) o->diag[k] = s[StatsCounters::kDiag + k];
-  if (!t->diag_build) {  // tail-compaction counters in diag 5-7 (used by the diagnostic builds otherwise)
-    o->diag[5] = s[StatsCounters::kResumedDrain];
-    o->diag[6] = s[StatsCounters::kTakeTries];
-    o->diag[7] = s[StatsCounters::kTakeSeen];
-  }
   o->launches = t->launches;
   o->kernel_ms = t->kernel_ms;
   o->gathers = t->gathers;

@@ -318,6 +318,34 @@ struct Flattener {
     for (size_t k = 0; k < kids.size(); k++) lind[4 * (off + 1 + k / 4) + k % 4] = Bits(kids[k]);
     return make_ref(kList, off);
   }
+  // A medium boundary that is a list of at most kBoundaryAAMax unit-normal axis-aligned quads (a box
+  // in its own space, MakeBox) also gets its children as consecutive QUADAA test words (8 words
+  // each, rt2_layout.h), right after the medium's record, so that a kernel loads the whole boundary
+  // at once with no child-ref indirection (two dependent scalar loads per quad and boundary query
+  // otherwise). Returns the medium record's word 3 (kBoundaryAAFlag | n << 24 | axis codes, 3 bits
+  // per child), or 0 (general path only). The general copy of the boundary is kept for kernels
+  // without the box path.
+  uint32_t BoundaryAA(int i, std::vector<float>& lind) {
+    const Obj& o = s.objs[(size_t)i];
+    if (o.kind != kList || o.children.empty() || o.children.size() > kBoundaryAAMax) return 0;
+    uint32_t codes = 0;
+    std::vector<float> words;
+    for (size_t k = 0; k < o.children.size(); k++) {
+      const int c = o.children[k];
+      if (s.objs[(size_t)c].kind != kQuad) return 0;
+      const float* r = out.nodes.data() + 4 * (size_t)(ref_of.at(c) & kOffsetMask);
+      uint32_t axis;
+      memcpy(&axis, &r[11], 4);
+      if (axis < 4 || axis > 6) return 0;
+      const int kk = (int)axis - 4, a = (kk + 1) % 3, b = (kk + 2) % 3;
+      // (sD, w[K], q[A], q[B], u[A], u[B], v[A], v[B]) of QUAD (n, D | q, mat | u, axis | v | w, sD)
+      const float rec[8] = {r[19], r[16 + kk], r[4 + a], r[4 + b], r[8 + a], r[8 + b], r[12 + a], r[12 + b]};
+      words.insert(words.end(), rec, rec + 8);
+      codes |= (axis - 4) << (3 * k);
+    }
+    lind.insert(lind.end(), words.begin(), words.end());
+    return kBoundaryAAFlag | ((uint32_t)o.children.size() << 24) | codes;
+  }
   // An accelerated list's tree in the threaded program: ACCBVH steps (padded box, skip = index
   // after the subtree) near child first, ACCSPHERE steps with aux = the sphere's record offset in
   // the node array, which is the list's child order (the kernel breaks equal roots by it).
@@ -387,6 +415,7 @@ struct Flattener {
       case kMedium: {
         if (ContainsAccList(o.child)) return false;  // boundary copies hold plain lists only
         uint32_t off = CopyRecords(src, kMediumRecords, lind);
+        lind[4 * off + 3] = Bits(BoundaryAA(o.child, lind));  // the box words follow the record
         uint32_t b = CopyBoundary(o.child, lind);
         lind[4 * off + 2] = Bits(b);
         emit(kMedium, off, 0);

@@ -415,25 +415,6 @@ struct PathT {
     seed_args(key0, key1, w);  // re-read at the refill (see karg16)
     philox(key0, key1, (xy >> 16) * w + (xy & 0xFFFFu), frame, b, w0, w1, w2, w3);
   }
-  // After a move to another lane (tail compaction): the buffer must hold the block of the last value
-  // drawn, (n - 1) >> 2 = n >> 2 unless n is a multiple of 4 (then the next draw refills anyway).
-  __device__ __forceinline__ void restore_block() {
-    if ((n & 3u) == 0u) return;
-    uint32_t w0, w1, w2, w3;
-    block(n >> 2, w0, w1, w2, w3);
-    if constexpr (kLdsRng) {
-      uint32_t* rb = rbw + __lane_id();
-      rb[0] = w0;
-      rb[64] = w1;
-      rb[128] = w2;
-      rb[192] = w3;
-    } else {
-      r0 = w0;
-      r1 = w1;
-      r2 = w2;
-      r3 = w3;
-    }
-  }
   // K consecutive uniforms in [0,1) (24-bit mantissa), in stream order
   template <int K>
   __device__ __forceinline__ void take(float* out) {
@@ -495,6 +476,35 @@ __device__ __forceinline__ void cos_sin_2pi(float v, float& c, float& s) {
   c = neg_c ? -cc : cc;
   s = neg_s ? -ss : ss;
 }
+// ln(u) of a 24-bit uniform (ConstantMedium.cpp:38 std::log(RandReal())): -inf at 0, else
+// e ln2 + log1p(f), u = 2^e (1 + f), 1 + f in [sqrt(1/2), sqrt(2)), log1p = f + f^2 Q(f) (degree-8 Q),
+// ln2 split so that e ln2_hi is exact; within 0.87 ulp of ln for every uniform. The oracle's LogU
+// evaluates the same operations in the same order (about 20 VALU instead of a double-precision log's
+// 40 plus its range handling).
+__device__ __forceinline__ float log_u(float u) {
+  if (u == 0.0f) return -__builtin_inff();
+  const uint32_t b = __float_as_uint(u);
+  int e = (int)(b >> 23) - 127;
+  float m = __uint_as_float((b & 0x007FFFFFu) | 0x3F800000u);
+  if (m > 1.41421354f) {
+    m = m * 0.5f;
+    e += 1;
+  }
+  const float f = m - 1.0f;
+  float q = -0.07477458566427231f;
+  q = fmaf(q, f, 0.12822002172470093f);
+  q = fmaf(q, f, -0.13261467218399048f);
+  q = fmaf(q, f, 0.1419624537229538f);
+  q = fmaf(q, f, -0.16608606278896332f);
+  q = fmaf(q, f, 0.2000119835138321f);
+  q = fmaf(q, f, -0.2500157654285431f);
+  q = fmaf(q, f, 0.3333333730697632f);
+  q = fmaf(q, f, -0.49999988079071045f);
+  const float l1p = fmaf(f * f, q, f);
+  const float ef = (float)e;
+  return fmaf(ef, 0.693145751953125f, fmaf(ef, 1.42860677e-06f, l1p));
+}
+
 // Math.hpp:26-43 RandUnitVec3 (uniform on the unit sphere) by the inverse-CDF map z = 1 - 2u,
 // phi = 2 pi v: two uniforms and no rejection loop, so a wave never waits on its unluckiest
 // lane's retries (the oracle draws the same map; DESIGN.md "Sampling").
@@ -852,7 +862,7 @@ __device__ __forceinline__ bool medium_t(const Nodes<kMode>& N, uint32_t off, f3
   t1 = fmaxf(t1, 0.0f);
   float len = sqrtf(dot(d, d));
   float inside = (t2 - t1) * len;
-  float hit_dist = r0.x * (float)log((double)path.uniform());
+  float hit_dist = r0.x * log_u(path.uniform());
   if (hit_dist > inside) return false;
   t_out = t1 + hit_dist / len;
   return true;
@@ -913,12 +923,69 @@ __device__ __forceinline__ bool boundary_t_lin(const void* recs, uint32_t ref, f
   return any;
 }
 
+// A box boundary (rt2_layout.h MEDIUM, kBoundaryAAFlag): the closest of its quads on [lo, hi], list
+// order, each by the unit-normal test with IEEE division: t = (sD - o_K) / d_K is exactly
+// Quad::Hit's (D - n.o) / (n.d) for n = +-e_K (negation commutes with rounding), the interior test is
+// quad_cand_aa's, and the interval test is Contains (inclusive).
+template <int K>
+__device__ __forceinline__ bool quad_aa_div(const uint32_t* r, f3 o, f3 d, float& t_out) {
+  constexpr int A = (K + 1) % 3, B = (K + 2) % 3;
+  const float dk = comp<K>(d);
+  const float t = (uf(r[0]) - comp<K>(o)) / dk;
+  const float pva = (comp<A>(o) + comp<A>(d) * t) - uf(r[2]);
+  const float pvb = (comp<B>(o) + comp<B>(d) * t) - uf(r[3]);
+  const float alpha = uf(r[1]) * (pva * uf(r[7]) - uf(r[6]) * pvb);
+  const float beta = uf(r[1]) * (uf(r[4]) * pvb - pva * uf(r[5]));
+  t_out = t;
+  return !(fabsf(dk) <= 1e-8f) && (0.0f <= alpha && alpha <= 1.0f) && (0.0f <= beta && beta <= 1.0f);
+}
+// The words come two quads (one 64-byte scalar load) at a time: no dependent loads, few SGPRs.
+__device__ __forceinline__ bool boundary_aa(const void* recs, uint32_t off, uint32_t hdr, f3 o, f3 d, float lo,
+                                            float hi, float& t_out, Counters& cnt) {
+  const uint32_t n = (hdr >> 24) & 7u;
+  bool any = false;
+  for (uint32_t k = 0; k < n; k += 2u) {  // wave-uniform
+    const u32x16 w = sld16(recs, off + 32u * k);
+#pragma unroll
+    for (uint32_t j = 0; j < 2u; j++) {
+      if (k + j < n) {
+        uint32_t r[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) r[i] = w[8 * j + i];
+        const uint32_t code = (hdr >> (3u * (k + j))) & 7u;
+        float t;
+        bool ok;
+        if (code == 0u) {
+          ok = quad_aa_div<0>(r, o, d, t);
+        } else if (code == 1u) {
+          ok = quad_aa_div<1>(r, o, d, t);
+        } else {
+          ok = quad_aa_div<2>(r, o, d, t);
+        }
+        cnt.quad++;
+        if (ok && lo <= t && t <= hi) {
+          any = true;
+          hi = t;
+        }
+      }
+    }
+  }
+  if (any) t_out = hi;
+  return any;
+}
+
 // medium_t with the boundary queries above (same operations, same random draw)
 template <uint32_t F, class G>
-__device__ __forceinline__ bool medium_t_lin(const void* recs, const u32x4 r0, f3 o, f3 d, float time, float tmin,
-                                             float tmax, G& path, float& t_out, Counters& cnt) {
+__device__ __forceinline__ bool medium_t_lin(const void* recs, uint32_t moff, const u32x4 r0, f3 o, f3 d, float time,
+                                             float tmin, float tmax, G& path, float& t_out, Counters& cnt) {
   const uint32_t bref = r0.z;
   float t1, t2;
+  // a box (the sphere scenes' kernels keep the general path: the 48 words cost them SGPRs)
+  if (!Has<F, kFeatSphere>() && (r0.w & kBoundaryAAFlag)) {
+    const uint32_t off = (moff + 1u) * 16u;
+    if (!boundary_aa(recs, off, r0.w, o, d, -FLT_MAX, FLT_MAX, t1, cnt)) return false;
+    if (!boundary_aa(recs, off, r0.w, o, d, (float)((double)t1 + 0.0001), FLT_MAX, t2, cnt)) return false;
+  } else {
 #if RT2_EXP_TWICE & 128
   {
     f3 o2 = o;
@@ -932,6 +999,7 @@ __device__ __forceinline__ bool medium_t_lin(const void* recs, const u32x4 r0, f
 #endif
   if (!boundary_t_lin<F>(recs, bref, o, d, time, -FLT_MAX, FLT_MAX, t1, cnt)) return false;
   if (!boundary_t_lin<F>(recs, bref, o, d, time, (float)((double)t1 + 0.0001), FLT_MAX, t2, cnt)) return false;
+  }
   t1 = fmaxf(t1, tmin);
   t2 = fminf(t2, tmax);
   if (t1 >= t2) return false;
@@ -943,11 +1011,11 @@ __device__ __forceinline__ bool medium_t_lin(const void* recs, const u32x4 r0, f
   {
     float u2 = u;
     asm volatile("" : "+v"(u2));
-    const float l2 = (float)log((double)u2);
+    const float l2 = log_u(u2);
     asm volatile("" ::"v"(l2));
   }
 #endif
-  float hit_dist = uf(r0.x) * (float)log((double)u);
+  float hit_dist = uf(r0.x) * log_u(u);
   if (hit_dist > inside) return false;
   t_out = t1 + hit_dist / len;
   return true;
@@ -1351,11 +1419,11 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, f3 wo, f3 wd
         G p2 = path;
         Counters c2 = cnt;
         float t2 = 0.0f;
-        const bool h2 = medium_t_lin<F>(recs, mr, o2, d, time, tmin, tmax, p2, t2, c2);
+        const bool h2 = medium_t_lin<F>(recs, off, mr, o2, d, time, tmin, tmax, p2, t2, c2);
         asm volatile("" ::"v"(t2), "v"((int)h2));
       }
 #endif
-      if (medium_t_lin<F>(recs, mr, o, d, time, tmin, tmax, path, t, cnt)) {
+      if (medium_t_lin<F>(recs, off, mr, o, d, time, tmin, tmax, path, t, cnt)) {
         tmax = t;
         prim = make_ref(kMedium, off);
         h.xf = cur_xf;
@@ -1543,62 +1611,6 @@ __device__ __forceinline__ uint32_t local_index(const LoopArgs& A, uint32_t xy) 
   return r * (uint32_t)A.width() + x;
 }
 
-// ------------------------------------------------------------------------------------------
-// Launch-tail compaction (RenderParams::migrants). Counters (work_counter[kMig*]) and entries are
-// shared by every workgroup of the launch across the 8 XCDs. Counters change only by single agent-scope
-// atomic adds / subtracts (no compare-and-swap loops: under contention those succeed once per memory
-// round trip) and are read by agent-scope atomic loads: `reserved` hands out entry slots to waves
-// moving paths out, `avail` counts published entries not yet claimed, `taken` hands out claimed slots
-// in order. Claims never exceed publications, and every slot below the publications is reserved, so a
-// claimed slot is written or being written. An entry is kMigrantWords 8-byte granules, each written by
-// one agent-scope atomic store as {epoch << 32 | word} and read by agent-scope atomic loads until every
-// granule carries this launch's epoch (self-validating: no fence or flag; the epoch is new every launch,
-// so earlier launches' entries never match).
-// Every shared word is accessed through a global (address space 1) pointer: flat instructions
-// would not carry the agent-scope cache policy the hand-off needs.
-enum : uint32_t { kMigReserved = 1, kMigTaken = 2, kMigAvail = 3 };  // work_counter words (0: items)
-typedef __attribute__((address_space(1))) uint32_t gu32;
-typedef __attribute__((address_space(1))) unsigned long long gu64;
-__device__ __forceinline__ gu32* gptr(uint32_t* p) { return (gu32*)p; }
-__device__ __forceinline__ uint32_t ld_agent(uint32_t* p) {
-  return __hip_atomic_load(gptr(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t add_agent(uint32_t* p, uint32_t v) {
-  return __hip_atomic_fetch_add(gptr(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t sub_agent(uint32_t* p, uint32_t v) {
-  return __hip_atomic_fetch_sub(gptr(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void migrant_put(unsigned long long* e, uint32_t epoch, const uint32_t (&w)[kMigrantWords]) {
-  gu64* const g = (gu64*)e;
-#pragma unroll
-  for (uint32_t k = 0; k < kMigrantWords; k++)
-    __hip_atomic_store(g + k, ((unsigned long long)epoch << 32) | w[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// Reads a claimed entry straight into the path state (word k -> *dst[k]), four granules at a time
-// (few registers beside the live paths' state), waiting for granules still in flight (bounded: false
-// after ~1 s, reported as an overflow; never expected).
-__device__ __forceinline__ bool migrant_take(unsigned long long* e, uint32_t epoch, bool& timeout,
-                                             uint32_t* const (&dst)[kMigrantWords]) {
-  for (uint32_t spin = 0; spin < (1u << 20); spin++) {
-    bool ok = true;
-#pragma unroll
-    for (uint32_t g = 0; g < kMigrantWords; g += 4) {
-#pragma unroll
-      for (uint32_t k = g; k < g + 4; k++) {
-        const unsigned long long x = __hip_atomic_load((gu64*)e + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *dst[k] = (uint32_t)x;
-        ok = ok && (uint32_t)(x >> 32) == epoch;
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (ok) return true;
-    __builtin_amdgcn_s_sleep(4);
-  }
-  timeout = true;
-  return false;
-}
-
 // Occupancy target (waves per SIMD the register allocation must allow), chosen per variant by
 // measurement (threaded kernels, round 2): Cornell 8 (7: -3 %), Cornell volume 7 (8 with the Philox
 // block in LDS: the same speed, more spill traffic), book 1 8, book 2 7 (6: -3 %; spills VGPRs, but
@@ -1664,7 +1676,6 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
                       // so the loop head is a convergence point and wave totals stay in SGPRs
   unsigned long long rays = 0;  // rays cast by the wave (popcounts of a ballot at the loop head)
   uint32_t bnext = 0, bend = 0;  // the wave's reserved batch of work items (wave-uniform)
-  bool dry = P.drain != 0u;      // the item queue is empty (wave-uniform; the drain launch has no items)
   uint32_t item_rays = 0;
   constexpr bool kLdsRng = LdsRng<F, kMode, kStats>();
   PathT<kLdsRng> path;
@@ -1701,195 +1712,7 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
   do {                 \
   } while (0)
 #endif
-  // ---- one iteration's bounce for every lane with a path (RayColor, RayTracer.cpp:20-45), then the
-  // sample of a finished frame; shared by the two phases below
-  auto bounce = [&]() {
-      rays += (unsigned long long)__popcll(__ballot(!need && (dl & 0xFFFFu) != 0u));  // RayColor casts below
-      if (need) return;
-      RT2_STAMP(st_fetch);
-
-      // ---- one bounce (RayColor, RayTracer.cpp:20-45)
-      bool done = false;
-      f3 color = mk(0, 0, 0);
-      if ((dl & 0xFFFFu) == 0u) {
-        done = true;  // RayColor(depth <= 0) returns 0 without casting a ray
-      } else {
-        if constexpr (kStats) item_rays++;
-        HitRef h;
-        bool hit;
-        if constexpr (kMode == kModeLinear) {
-          hit = trace_linear<F, kStats>(P, ro, rd, rtime, path, h, cnt);
-  #if RT2_EXP_TRACE_TWICE
-          {
-            f3 ro2 = ro;
-            asm volatile("" : "+v"(ro2.x), "+v"(ro2.y), "+v"(ro2.z));
-            HitRef h2;
-            auto p2 = path;
-            bool hit2 = trace_linear<F, kStats>(P, ro2, rd, rtime, p2, h2, cnt);
-            asm volatile("" ::"v"(h2.t), "v"(h2.prim), "v"(h2.xf), "v"((int)hit2));
-          }
-  #endif
-        } else {
-          hit = trace_stack<F, kMode, kStats>(P, N, ro, rd, rtime, path, h, stk, cnt, overflow);
-        }
-        RT2_STAMP(st_trace);
-        if (!hit) {
-          color = thr * bg;
-          done = true;
-        } else {
-          f3 hp, hn;
-          bool front;
-          uint32_t mat;
-          if constexpr (kMode == kModeLinear) {
-            resolve_hit<F>(Nodes<kModeLinear>{reinterpret_cast<const float4*>(P.lind)}, h, ro, rd, rtime, hp, hn, front,
-                           mat);
-  #if RT2_EXP_TWICE & 1
-            {
-              f3 ro2 = ro, hp2, hn2;
-              bool fr2;
-              uint32_t m2;
-              asm volatile("" : "+v"(ro2.x), "+v"(ro2.y), "+v"(ro2.z));
-              resolve_hit<F>(Nodes<kModeLinear>{reinterpret_cast<const float4*>(P.lind)}, h, ro2, rd, rtime, hp2, hn2,
-                             fr2, m2);
-              asm volatile("" ::"v"(hp2.x), "v"(hp2.y), "v"(hp2.z), "v"(hn2.x), "v"(hn2.y), "v"(hn2.z), "v"(m2),
-                           "v"((int)fr2));
-            }
-  #endif
-          } else {
-            resolve_hit<F>(N, h, ro, rd, rtime, hp, hn, front, mat);
-          }
-          const ShadeArgs S = shade_args();
-          float4 m0 = S.materials[2 * mat], m1 = S.materials[2 * mat + 1];
-          uint32_t type = bits(m0.x);
-          if (type == kMatDiffuseLight) {
-            color = thr * tex_value<F>(S, bits(m1.z), hp);
-            done = true;
-          } else {
-            f3 att, dir;
-            bool dielectric = Has<F, kFeatSpecular>() && type == kMatDielectric;
-            f3 ru = mk(0.0f, 0.0f, 0.0f);
-            if (!dielectric) ru = rand_unit_vec3(path);  // one sampling site for every other material
-  #if RT2_EXP_TWICE & 2
-            {
-              auto p2 = path;
-              asm volatile("" : "+v"(p2.n), "+v"(p2.frame));
-              f3 r2 = rand_unit_vec3(p2);
-              asm volatile("" ::"v"(r2.x), "v"(r2.y), "v"(r2.z));
-            }
-  #endif
-            if (Has<F, kFeatSpecular>() && type == kMatMetal) {
-              dir = normalize(reflect(rd, hn)) + (m1.x * ru);
-              att = mk(m0.y, m0.z, m0.w);
-            } else if (dielectric) {
-              att = mk(1.0f, 1.0f, 1.0f);
-              float ri = front ? m1.w : m1.y;
-              f3 ud = normalize(rd);
-              float cos_t = gmin(dot(-ud, hn), 1.0f);
-              float sin_t = sqrtf(1.0f - cos_t * cos_t);
-              bool refl = ri * sin_t > 1.0f;
-              if (!refl) {
-                float r0 = (1.0f - ri) / (1.0f + ri);
-                r0 = r0 * r0;
-                double xx = (double)(1.0f - cos_t);
-                double x2 = xx * xx;
-                double x5 = (x2 * x2) * xx;
-                double schlick = (double)r0 + (double)(1.0f - r0) * x5;
-                refl = schlick > (double)path.uniform();
-              }
-              dir = refl ? reflect(ud, hn) : refract(ud, hn, ri);
-            } else if (Has<F, kFeatMedium>() && type == kMatIsotropic) {
-              dir = ru;
-              att = tex_value<F>(S, bits(m1.z), hp);
-            } else {  // Lambertian / Texture
-              dir = hn + ru;
-              if (near_zero(dir)) dir = hn;
-              att = (type == kMatLambertian) ? mk(m0.y, m0.z, m0.w) : tex_value<F>(S, bits(m1.z), hp);
-            }
-            thr = thr * att;
-            ro = hp;
-            rd = dir;
-            dl--;  // depth_left > 0 here: no borrow into the frame count
-          }
-        }
-      }
-      RT2_STAMP(st_shade);
-      if (done) {
-        // this frame's sample, summed in frame order by accumulate_kernel (RayTracer.cpp:64)
-        const LoopArgs A = loop_args();
-        const uint32_t lidx = local_index(A, path.xy);
-        const uint32_t fr = path.frame - (uint32_t)A.frame_begin();  // launch-relative frame
-        const uint32_t slot = fr & (kOctet - 1u);
-        float* blk = A.samples() + 3ull * kOctet * ((unsigned long long)(fr / kOctet) * A.local_pixels() + lidx);
-        const bool more = ((dl >> 16) & kChunkLeftMask) != 0u;  // frames of the chunk after this one
-        if constexpr (kGroup != 0u) {
-          float* oct = oct_wave + __lane_id();
-          const uint32_t gs = slot & (kGroup - 1u);  // slot within the group = LDS slot
-          if (gs == kGroup - 1u || !more) {
-            const uint32_t g0 = slot - gs;  // the group's first octet slot
-            const uint32_t first = max(dl >> 27, g0) - g0;  // this lane's first LDS slot of the group
-            if (first == 0u && gs == kGroup - 1u) {  // the whole group: 16-B stores
-              float4* b4 = reinterpret_cast<float4*>(blk + 3u * g0);
-  #pragma unroll
-              for (uint32_t j = 0; j + 1u < 3u * kGroup / 4u; j++)  // planes 4j..4j+3, few live registers
-                b4[j] = make_float4(oct[64u * (4u * j)], oct[64u * (4u * j + 1u)], oct[64u * (4u * j + 2u)],
-                                    oct[64u * (4u * j + 3u)]);
-              b4[3u * kGroup / 4u - 1u] = make_float4(oct[64u * (kPlanes - 1u)], color.x, color.y, color.z);
-            } else {  // a chunk edge inside the group: this lane's slots first..gs
-              for (uint32_t k = first; k < gs; k++) {
-                blk[3u * (g0 + k)] = oct[64u * (3u * k)];
-                blk[3u * (g0 + k) + 1u] = oct[64u * (3u * k + 1u)];
-                blk[3u * (g0 + k) + 2u] = oct[64u * (3u * k + 2u)];
-              }
-              blk[3u * slot] = color.x;
-              blk[3u * slot + 1u] = color.y;
-              blk[3u * slot + 2u] = color.z;
-            }
-          } else {
-            oct[64u * (3u * gs)] = color.x;
-            oct[64u * (3u * gs + 1u)] = color.y;
-            oct[64u * (3u * gs + 2u)] = color.z;
-          }
-        } else {
-          blk[3u * slot] = color.x;
-          blk[3u * slot + 1u] = color.y;
-          blk[3u * slot + 2u] = color.z;
-        }
-        int f = (int)path.frame + 1;
-        if (more) {
-          path.start((uint32_t)f);
-          {  // next stratum: (f % sq, f / sq % sq) from the previous frame's
-            const uint32_t sq = (uint32_t)P.cam.sqrt_spp;
-            uint32_t si = (path.sij & 0xFFFFu) + 1u, sj = path.sij >> 16;
-            if (si == sq) {
-              si = 0u;
-              sj = sj + 1u == sq ? 0u : sj + 1u;
-            }
-            path.sij = si | (sj << 16);
-          }
-  #if RT2_EXP_TWICE & 4
-          {
-            auto p2 = path;
-            f3 o2, d2;
-            float t2;
-            asm volatile("" : "+v"(p2.frame), "+v"(p2.sij));
-            camera_ray<F>(P, p2, o2, d2, t2);
-            asm volatile("" ::"v"(o2.x), "v"(d2.x), "v"(d2.y), "v"(d2.z), "v"(t2));
-          }
-  #endif
-          camera_ray<F>(P, path, ro, rd, rtime);
-          thr = mk(1, 1, 1);
-          // one frame fewer left; after the octet's last slot the next octet starts at slot 0
-          dl = (((dl & 0x07FF0000u) - 0x10000u) | (uint32_t)A.max_depth()) | (slot == kOctet - 1u ? 0u : (dl & 0xF8000000u));
-        } else {
-          if (kStats && P.ray_counts) atomicAdd(P.ray_counts + lidx, item_rays);
-          need = true;
-        }
-      }
-      RT2_STAMP(st_finish);
-  };
-
-  // ---- phase 1: work items from the launch's queue
-  while (!dry) {
+  while (true) {
 #if RT2_EXP_STAMPS
     st_t = __builtin_amdgcn_s_memtime();
 #endif
@@ -1898,7 +1721,11 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
     // work left (guided self-scheduling), so the counter sees few atomics early and the last
     // items still spread over all waves.
     unsigned long long mask = __ballot(need && !idle);
-    if (mask != 0ull) {
+    // a lane of this wave found the items exhausted (handed out in order: none are left); the
+    // others stop asking (no more atomics on the work counter in the launch's tail)
+    if (mask != 0ull && __ballot(idle) != 0ull) {
+      if (need) idle = true;
+    } else if (mask != 0ull) {
       const LoopArgs A = loop_args();
       const uint32_t max_depth = (uint32_t)A.max_depth();  // <= 0xFFFF (rt2_tracer_set_max_depth)
       const uint32_t count = (uint32_t)__popcll(mask);
@@ -1976,133 +1803,193 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
           }
         }
       }
-      dry = __ballot(idle) != 0ull;  // items are handed out in order: one past the end means none left
     }
 #if RT2_EXP_ENDTIME
     if (et_idle == 0ull && __ballot(idle) != 0ull) et_idle = __builtin_amdgcn_s_memrealtime();
 #endif
-    if (dry) break;  // phase 2 (the lanes' paths are kept)
-    bounce();
-  }
-
-  // ---- phase 2, launch tail: no items left. Paths move between waves so that the lanes still
-  // tracing stay packed (RayTracer.cpp:69's work-stealing loop keeps every worker busy to the end):
-  // lanes that finished take queued paths; a wave left with at most tail_min paths and nothing to
-  // take moves them to the queue and exits; the drain launch takes what is still queued. A path's
-  // arithmetic and random stream do not depend on the lane that runs it: results are bit-identical.
-  bool fresh = true;  // lanes freed by phase 1's last fetch
-  while (true) {
-    const unsigned long long fin = __ballot(need && !idle);  // lanes whose path ended last iteration
-    if (need) idle = true;
-#if RT2_EXP_ENDTIME
-    if (et_idle == 0ull && __ballot(idle) != 0ull) et_idle = __builtin_amdgcn_s_memrealtime();
-#endif
-    static_assert(RT2_KOFF(epoch) == RT2_KOFF(mcap) + 4 && RT2_KOFF(tail_min) == RT2_KOFF(mcap) + 8 &&
-                      RT2_KOFF(drain) == RT2_KOFF(mcap) + 12, "RenderParams layout");
-    const u32x4 tp = karg4<RT2_KOFF(mcap)>();  // mcap, epoch, tail_min, drain
-    const unsigned long long freem = __ballot(idle);
-#ifndef RT2_TAIL_TAKE_MIN
-#define RT2_TAIL_TAKE_MIN 1
-#endif
-    if ((tp[2] | tp[3]) != 0u && (fin != 0ull || fresh) && __popcll(freem) >= (tp[3] ? 1 : RT2_TAIL_TAKE_MIN)) {
-      // take queued paths into the free lanes: claim up to `want` of the published entries (the
-      // `avail` count, taken down first and given back where it fell short), then the next entries
-      // in claim order. Every entry below the claims is reserved, so an entry not yet written is
-      // being written now (migrant_take waits for it).
-      // (pointers re-read from the argument segment here, not held across the loops: see karg16)
-      static_assert(RT2_KOFF(stats) == RT2_KOFF(work_counter) + 8, "RenderParams layout");
-      const u32x4 wp = karg4<RT2_KOFF(work_counter)>();
-      uint32_t* const wctr = reinterpret_cast<uint32_t*>((unsigned long long)wp[0] | ((unsigned long long)wp[1] << 32));
-      uint32_t first = 0, k = 0;
-      bool seen = false;
-      if (lane == __builtin_amdgcn_readfirstlane(lane) && (seen = (int)ld_agent(wctr + kMigAvail) > 0)) {
-        const int want = __popcll(freem);
-        const int o = (int)sub_agent(wctr + kMigAvail, (uint32_t)want);
-        const int c = o <= 0 ? 0 : (o < want ? o : want);
-        if (c < want) add_agent(wctr + kMigAvail, (uint32_t)(want - c));
-        if (c > 0) first = add_agent(wctr + kMigTaken, (uint32_t)c);
-        k = (uint32_t)c;
-      }
-      k = __builtin_amdgcn_readfirstlane(k);
-      first = __builtin_amdgcn_readfirstlane(first);
-      const uint32_t rank = (uint32_t)__popcll(freem & ((1ull << lane) - 1ull));
-      if (k != 0u && idle && rank < k) {
-        unsigned long long* const migrants = reinterpret_cast<unsigned long long*>(karg2<RT2_KOFF(migrants)>());
-        uint32_t* const dst[kMigrantWords] = {
-            reinterpret_cast<uint32_t*>(&ro.x),  reinterpret_cast<uint32_t*>(&ro.y),  reinterpret_cast<uint32_t*>(&ro.z),
-            reinterpret_cast<uint32_t*>(&rd.x),  reinterpret_cast<uint32_t*>(&rd.y),  reinterpret_cast<uint32_t*>(&rd.z),
-            reinterpret_cast<uint32_t*>(&thr.x), reinterpret_cast<uint32_t*>(&thr.y), reinterpret_cast<uint32_t*>(&thr.z),
-            reinterpret_cast<uint32_t*>(&rtime), &dl, &path.frame, &path.xy, &path.sij, &path.n, &item_rays};
-        if (migrant_take(migrants + (unsigned long long)kMigrantWords * (first + rank), tp[1], overflow, dst)) {
-          path.restore_block();
-          idle = false;
-          need = false;
-        }
-      }
-      const unsigned long long got = __ballot(!need) & freem;
-      if (got != 0ull && lane == __builtin_amdgcn_readfirstlane(lane)) {
-        unsigned long long* const stats = reinterpret_cast<unsigned long long*>((unsigned long long)wp[2] |
-                                                                               ((unsigned long long)wp[3] << 32));
-        atomicAdd(stats + (tp[3] ? StatsCounters::kResumedDrain : StatsCounters::kResumed), (unsigned long long)__popcll(got));
-      }
-      if (lane == __builtin_amdgcn_readfirstlane(lane)) {  // diagnostic counts
-        unsigned long long* const stats = reinterpret_cast<unsigned long long*>((unsigned long long)wp[2] |
-                                                                               ((unsigned long long)wp[3] << 32));
-        atomicAdd(stats + StatsCounters::kTakeTries, 1ull);
-        if (seen) atomicAdd(stats + StatsCounters::kTakeSeen, 1ull);
-      }
-    }
-    fresh = false;
-    const unsigned long long live = __ballot(!need);
-    const uint32_t nlive = (uint32_t)__popcll(live);
-    if (tp[3] == 0u && nlive != 0u && nlive <= tp[2]) {  // few paths left: move them to the queue, exit
-      static_assert(RT2_KOFF(stats) == RT2_KOFF(work_counter) + 8, "RenderParams layout");
-      const u32x4 wp = karg4<RT2_KOFF(work_counter)>();
-      uint32_t* const wctr = reinterpret_cast<uint32_t*>((unsigned long long)wp[0] | ((unsigned long long)wp[1] << 32));
-      // reserve entries [first, first + nlive) below the capacity (a reservation past it keeps its
-      // paths: later reservations only lie further out, so no claim ever reaches it)
-      uint32_t first = 0xFFFFFFFFu;
-      if (lane == __builtin_amdgcn_readfirstlane(lane) && ld_agent(wctr + kMigReserved) + nlive <= tp[0]) {
-        first = add_agent(wctr + kMigReserved, nlive);
-        if (first + nlive > tp[0]) first = 0xFFFFFFFFu;
-      }
-      first = __builtin_amdgcn_readfirstlane(first);
-      if (first != 0xFFFFFFFFu) {
-        if (!need) {
-          if constexpr (kGroup != 0u) {
-            // this group's samples held in LDS are written now (the new lane starts its staging at
-            // the current frame's slot)
-            const LoopArgs A = loop_args();
-            const uint32_t lidx = local_index(A, path.xy);
-            const uint32_t fr = path.frame - (uint32_t)A.frame_begin();
-            const uint32_t slot = fr & (kOctet - 1u), gs = slot & (kGroup - 1u), g0 = slot - gs;
-            float* blk = A.samples() + 3ull * kOctet * ((unsigned long long)(fr / kOctet) * A.local_pixels() + lidx);
-            const float* oct = oct_wave + __lane_id();
-            for (uint32_t j = max(dl >> 27, g0) - g0; j < gs; j++) {
-              blk[3u * (g0 + j)] = oct[64u * (3u * j)];
-              blk[3u * (g0 + j) + 1u] = oct[64u * (3u * j + 1u)];
-              blk[3u * (g0 + j) + 2u] = oct[64u * (3u * j + 2u)];
-            }
-            dl = (dl & 0x07FFFFFFu) | (slot << 27);
-          }
-          const uint32_t w[kMigrantWords] = {bits(ro.x), bits(ro.y), bits(ro.z), bits(rd.x), bits(rd.y), bits(rd.z),
-                                             bits(thr.x), bits(thr.y), bits(thr.z), bits(rtime), dl, path.frame,
-                                             path.xy, path.sij, path.n, item_rays};
-          unsigned long long* const migrants = reinterpret_cast<unsigned long long*>(karg2<RT2_KOFF(migrants)>());
-          migrant_put(migrants + (unsigned long long)kMigrantWords * (first + (uint32_t)__popcll(live & ((1ull << lane) - 1ull))),
-                      tp[1], w);
-        }
-        if (lane == __builtin_amdgcn_readfirstlane(lane)) {
-          add_agent(wctr + kMigAvail, nlive);  // published (takers wait for entries still in flight)
-          unsigned long long* const stats = reinterpret_cast<unsigned long long*>((unsigned long long)wp[2] |
-                                                                                 ((unsigned long long)wp[3] << 32));
-          atomicAdd(stats + StatsCounters::kMigrated, (unsigned long long)nlive);
-        }
-        break;  // every lane: the wave is done, its paths continue on other lanes
-      }
-    }
     if (__ballot(!idle) == 0ull) break;  // the wave is done (uniform exit)
-    bounce();
+    rays += (unsigned long long)__popcll(__ballot(!need && (dl & 0xFFFFu) != 0u));  // RayColor casts below
+    if (need) continue;
+    RT2_STAMP(st_fetch);
+
+    // ---- one bounce (RayColor, RayTracer.cpp:20-45)
+    bool done = false;
+    f3 color = mk(0, 0, 0);
+    if ((dl & 0xFFFFu) == 0u) {
+      done = true;  // RayColor(depth <= 0) returns 0 without casting a ray
+    } else {
+      if constexpr (kStats) item_rays++;
+      HitRef h;
+      bool hit;
+      if constexpr (kMode == kModeLinear) {
+        hit = trace_linear<F, kStats>(P, ro, rd, rtime, path, h, cnt);
+#if RT2_EXP_TRACE_TWICE
+        {
+          f3 ro2 = ro;
+          asm volatile("" : "+v"(ro2.x), "+v"(ro2.y), "+v"(ro2.z));
+          HitRef h2;
+          auto p2 = path;
+          bool hit2 = trace_linear<F, kStats>(P, ro2, rd, rtime, p2, h2, cnt);
+          asm volatile("" ::"v"(h2.t), "v"(h2.prim), "v"(h2.xf), "v"((int)hit2));
+        }
+#endif
+      } else {
+        hit = trace_stack<F, kMode, kStats>(P, N, ro, rd, rtime, path, h, stk, cnt, overflow);
+      }
+      RT2_STAMP(st_trace);
+      if (!hit) {
+        color = thr * bg;
+        done = true;
+      } else {
+        f3 hp, hn;
+        bool front;
+        uint32_t mat;
+        if constexpr (kMode == kModeLinear) {
+          resolve_hit<F>(Nodes<kModeLinear>{reinterpret_cast<const float4*>(P.lind)}, h, ro, rd, rtime, hp, hn, front,
+                         mat);
+#if RT2_EXP_TWICE & 1
+          {
+            f3 ro2 = ro, hp2, hn2;
+            bool fr2;
+            uint32_t m2;
+            asm volatile("" : "+v"(ro2.x), "+v"(ro2.y), "+v"(ro2.z));
+            resolve_hit<F>(Nodes<kModeLinear>{reinterpret_cast<const float4*>(P.lind)}, h, ro2, rd, rtime, hp2, hn2,
+                           fr2, m2);
+            asm volatile("" ::"v"(hp2.x), "v"(hp2.y), "v"(hp2.z), "v"(hn2.x), "v"(hn2.y), "v"(hn2.z), "v"(m2),
+                         "v"((int)fr2));
+          }
+#endif
+        } else {
+          resolve_hit<F>(N, h, ro, rd, rtime, hp, hn, front, mat);
+        }
+        const ShadeArgs S = shade_args();
+        float4 m0 = S.materials[2 * mat], m1 = S.materials[2 * mat + 1];
+        uint32_t type = bits(m0.x);
+        if (type == kMatDiffuseLight) {
+          color = thr * tex_value<F>(S, bits(m1.z), hp);
+          done = true;
+        } else {
+          f3 att, dir;
+          bool dielectric = Has<F, kFeatSpecular>() && type == kMatDielectric;
+          f3 ru = mk(0.0f, 0.0f, 0.0f);
+          if (!dielectric) ru = rand_unit_vec3(path);  // one sampling site for every other material
+#if RT2_EXP_TWICE & 2
+          {
+            auto p2 = path;
+            asm volatile("" : "+v"(p2.n), "+v"(p2.frame));
+            f3 r2 = rand_unit_vec3(p2);
+            asm volatile("" ::"v"(r2.x), "v"(r2.y), "v"(r2.z));
+          }
+#endif
+          if (Has<F, kFeatSpecular>() && type == kMatMetal) {
+            dir = normalize(reflect(rd, hn)) + (m1.x * ru);
+            att = mk(m0.y, m0.z, m0.w);
+          } else if (dielectric) {
+            att = mk(1.0f, 1.0f, 1.0f);
+            float ri = front ? m1.w : m1.y;
+            f3 ud = normalize(rd);
+            float cos_t = gmin(dot(-ud, hn), 1.0f);
+            float sin_t = sqrtf(1.0f - cos_t * cos_t);
+            bool refl = ri * sin_t > 1.0f;
+            if (!refl) {
+              float r0 = (1.0f - ri) / (1.0f + ri);
+              r0 = r0 * r0;
+              double xx = (double)(1.0f - cos_t);
+              double x2 = xx * xx;
+              double x5 = (x2 * x2) * xx;
+              double schlick = (double)r0 + (double)(1.0f - r0) * x5;
+              refl = schlick > (double)path.uniform();
+            }
+            dir = refl ? reflect(ud, hn) : refract(ud, hn, ri);
+          } else if (Has<F, kFeatMedium>() && type == kMatIsotropic) {
+            dir = ru;
+            att = tex_value<F>(S, bits(m1.z), hp);
+          } else {  // Lambertian / Texture
+            dir = hn + ru;
+            if (near_zero(dir)) dir = hn;
+            att = (type == kMatLambertian) ? mk(m0.y, m0.z, m0.w) : tex_value<F>(S, bits(m1.z), hp);
+          }
+          thr = thr * att;
+          ro = hp;
+          rd = dir;
+          dl--;  // depth_left > 0 here: no borrow into the frame count
+        }
+      }
+    }
+    RT2_STAMP(st_shade);
+    if (done) {
+      // this frame's sample, summed in frame order by accumulate_kernel (RayTracer.cpp:64)
+      const LoopArgs A = loop_args();
+      const uint32_t lidx = local_index(A, path.xy);
+      const uint32_t fr = path.frame - (uint32_t)A.frame_begin();  // launch-relative frame
+      const uint32_t slot = fr & (kOctet - 1u);
+      float* blk = A.samples() + 3ull * kOctet * ((unsigned long long)(fr / kOctet) * A.local_pixels() + lidx);
+      const bool more = ((dl >> 16) & kChunkLeftMask) != 0u;  // frames of the chunk after this one
+      if constexpr (kGroup != 0u) {
+        float* oct = oct_wave + __lane_id();
+        const uint32_t gs = slot & (kGroup - 1u);  // slot within the group = LDS slot
+        if (gs == kGroup - 1u || !more) {
+          const uint32_t g0 = slot - gs;  // the group's first octet slot
+          const uint32_t first = max(dl >> 27, g0) - g0;  // this lane's first LDS slot of the group
+          if (first == 0u && gs == kGroup - 1u) {  // the whole group: 16-B stores
+            float4* b4 = reinterpret_cast<float4*>(blk + 3u * g0);
+#pragma unroll
+            for (uint32_t j = 0; j + 1u < 3u * kGroup / 4u; j++)  // planes 4j..4j+3, few live registers
+              b4[j] = make_float4(oct[64u * (4u * j)], oct[64u * (4u * j + 1u)], oct[64u * (4u * j + 2u)],
+                                  oct[64u * (4u * j + 3u)]);
+            b4[3u * kGroup / 4u - 1u] = make_float4(oct[64u * (kPlanes - 1u)], color.x, color.y, color.z);
+          } else {  // a chunk edge inside the group: this lane's slots first..gs
+            for (uint32_t k = first; k < gs; k++) {
+              blk[3u * (g0 + k)] = oct[64u * (3u * k)];
+              blk[3u * (g0 + k) + 1u] = oct[64u * (3u * k + 1u)];
+              blk[3u * (g0 + k) + 2u] = oct[64u * (3u * k + 2u)];
+            }
+            blk[3u * slot] = color.x;
+            blk[3u * slot + 1u] = color.y;
+            blk[3u * slot + 2u] = color.z;
+          }
+        } else {
+          oct[64u * (3u * gs)] = color.x;
+          oct[64u * (3u * gs + 1u)] = color.y;
+          oct[64u * (3u * gs + 2u)] = color.z;
+        }
+      } else {
+        blk[3u * slot] = color.x;
+        blk[3u * slot + 1u] = color.y;
+        blk[3u * slot + 2u] = color.z;
+      }
+      int f = (int)path.frame + 1;
+      if (more) {
+        path.start((uint32_t)f);
+        {  // next stratum: (f % sq, f / sq % sq) from the previous frame's
+          const uint32_t sq = (uint32_t)P.cam.sqrt_spp;
+          uint32_t si = (path.sij & 0xFFFFu) + 1u, sj = path.sij >> 16;
+          if (si == sq) {
+            si = 0u;
+            sj = sj + 1u == sq ? 0u : sj + 1u;
+          }
+          path.sij = si | (sj << 16);
+        }
+#if RT2_EXP_TWICE & 4
+        {
+          auto p2 = path;
+          f3 o2, d2;
+          float t2;
+          asm volatile("" : "+v"(p2.frame), "+v"(p2.sij));
+          camera_ray<F>(P, p2, o2, d2, t2);
+          asm volatile("" ::"v"(o2.x), "v"(d2.x), "v"(d2.y), "v"(d2.z), "v"(t2));
+        }
+#endif
+        camera_ray<F>(P, path, ro, rd, rtime);
+        thr = mk(1, 1, 1);
+        // one frame fewer left; after the octet's last slot the next octet starts at slot 0
+        dl = (((dl & 0x07FF0000u) - 0x10000u) | (uint32_t)A.max_depth()) | (slot == kOctet - 1u ? 0u : (dl & 0xF8000000u));
+      } else {
+        if (kStats && P.ray_counts) atomicAdd(P.ray_counts + lidx, item_rays);
+        need = true;
+      }
+    }
+    RT2_STAMP(st_finish);
   }
 
 #if RT2_EXP_STAMPS

@@ -79,6 +79,11 @@ inline constexpr uint32_t make_ref(uint32_t kind, uint32_t off) { return (kind <
 //  XFORM : (invM col0.xyz, child_ref bits) (invM col1.xyz, parent_xform_ref bits)
 //          (invM col2.xyz, 0) (invM col3.xyz, 0) (M col0.xyz,0) (M col1.xyz,0) (M col2.xyz,0) (M col3.xyz,0)
 //  MEDIUM: (neg_inv_density, material bits, boundary_ref bits, 0)
+//          In the threaded program's record copy, a boundary that is a list of at most
+//          kBoundaryAAMax unit-normal axis-aligned quads (a box in the medium's space) also has its
+//          children's 8-word QUADAA test records right after the medium record, and word 3 =
+//          kBoundaryAAFlag | count << 24 | (axis K of child k) << 3k (boundary_ref keeps the
+//          general copy).
 //  LISTACC: (center.xyz, R) (k2, k1, k0, root_ref bits): a HittableList of n >= kListAccelMin
 //          spheres (HittableList.cpp:8-22). The list returns the smallest accepted root and, on
 //          equal roots, its first child (Sphere uses the strict Surrounds), so any visiting
@@ -92,6 +97,8 @@ inline constexpr uint32_t make_ref(uint32_t kind, uint32_t off) { return (kind <
 //          centroids along the node's split axis (kind - kAccBvh); children are ACCBVH or
 //          ACCSPHERE refs (an ACCSPHERE ref points at the child's SPHERE record)
 constexpr uint32_t kListLeafOnly = 1u;
+constexpr uint32_t kBoundaryAAFlag = 0x80000000u;
+constexpr uint32_t kBoundaryAAMax = 6;
 
 constexpr int kBvhRecords = 2, kQuadRecords = 5, kSphereRecords = 2, kXformRecords = 8, kMediumRecords = 1;
 
@@ -170,10 +177,7 @@ struct CameraParams {
 
 struct StatsCounters {  // u64 slots written by the kernel
   enum { kRays = 0, kBvhTests, kQuadTests, kSphereTests, kXformVisits, kMediumTests, kListVisits, kPaths, kCount };
-  // stamps / diag: diagnostic builds; tail compaction: paths moved, taken in the launch, taken by
-  // the drain launch, take attempts, attempts that saw published paths
-  enum { kOverflow = kCount, kStamps = 9, kMigrated = 13, kResumed = 14, kResumedDrain = 15, kDiag = 16,
-         kTakeTries = 24, kTakeSeen = 25, kSlots = 32 };
+  enum { kOverflow = kCount, kStamps = 9, kDiag = 16, kSlots = 32 };  // stamps / diag: diagnostic builds
 };
 constexpr int kStatsSlots = StatsCounters::kSlots;
 
@@ -241,16 +245,6 @@ struct RenderParams {
   uint32_t frame_tiles;
   uint32_t frame_tile;
   Magic div_frame_tile, div_width;
-  // Launch-tail compaction (the item queue is empty; RayTracer.cpp:69's work stealing keeps every
-  // worker busy to the end, this keeps every lane busy): a wave with at most tail_min paths left
-  // moves them to the migrant queue and exits; waves with free lanes take queued paths; a drain
-  // launch (drain = 1: no items, no moves) finishes what is left. An entry is kMigrantWords 8-byte
-  // granules {epoch << 32 | word} (self-validating: written and read with no other ordering);
-  // work_counter[1] = entries reserved, work_counter[2] = entries taken. tail_min 0: off.
-  unsigned long long* migrants;
-  uint32_t mcap, epoch, tail_min, drain;
 };
-constexpr uint32_t kMigrantWords = 16;  // ray origin, direction, throughput, time, depth/frames, frame,
-                                        // pixel, stratum, RNG draw count, the item's rays
 
 }  // namespace rt2

@@ -366,10 +366,6 @@ class RayTracer:
     def set_sample_budget(self, nbytes: int) -> None:
         check(lib.rt2_tracer_set_sample_budget(self._h, int(nbytes)))
 
-    def set_tail_compaction(self, min_paths: int) -> None:
-        """Launch-tail compaction threshold (rt2_tracer_set_tail_compaction; 0 = off)."""
-        check(lib.rt2_tracer_set_tail_compaction(self._h, int(min_paths)))
-
     def set_batch_max(self, items: int) -> None:
         check(lib.rt2_tracer_set_batch_max(self._h, int(items)))
 

@@ -7,7 +7,7 @@ SEED = 0x5EED2024
 
 
 def _gpu_render_once(name, w, h, spp, frames, *, seed, max_depth, band_h, rank, world, launch_frames, updates,
-                     stats, work_split, sample_budget, batch_max, ray_counts, lazy, tail=None):
+                     stats, work_split, sample_budget, batch_max, ray_counts, lazy):
     import torch  # noqa: F401
     import raytrace2_amd as R
     sc = R.Scene(scene_path(name), seed)
@@ -32,8 +32,6 @@ def _gpu_render_once(name, w, h, spp, frames, *, seed, max_depth, band_h, rank, 
         tr.set_batch_max(batch_max)
     if lazy is not None:
         tr.set_lazy_frames(lazy)
-    if tail is not None:
-        tr.set_tail_compaction(tail)
     if updates:
         for _ in range(frames):
             tr.Update(sc)
@@ -49,13 +47,12 @@ def _gpu_render_once(name, w, h, spp, frames, *, seed, max_depth, band_h, rank, 
 
 def gpu_render(name, w, h, spp, frames, *, seed=SEED, max_depth=50, band_h=0, rank=0, world=1,
                launch_frames=0, updates=False, stats=False, work_split=None, sample_budget=None, batch_max=None,
-               counts=True, lazy=None, tail=None):
+               counts=True, lazy=None):
     """Renders with the product kernel (no per-pixel counters) and, when `counts`, again with the
     counting kernel (per-pixel ray counts); the two must agree bit for bit. Returns the product
     render's (accumulation, ray counts of the counting render or None, stats, pixels)."""
     kw = dict(seed=seed, max_depth=max_depth, band_h=band_h, rank=rank, world=world, launch_frames=launch_frames,
-              updates=updates, work_split=work_split, sample_budget=sample_budget, batch_max=batch_max, lazy=lazy,
-              tail=tail)
+              updates=updates, work_split=work_split, sample_budget=sample_budget, batch_max=batch_max, lazy=lazy)
     acc, _, st, px = _gpu_render_once(name, w, h, spp, frames, stats=stats, ray_counts=False, **kw)
     rc = None
     if counts:
@@ -64,7 +61,6 @@ def gpu_render(name, w, h, spp, frames, *, seed=SEED, max_depth=50, band_h=0, ra
         assert np.array_equal(px, px2)
         assert st["rays"] == st2["rays"] == int(rc.astype(np.uint64).sum()), (st["rays"], st2["rays"])
         assert st["paths"] == st2["paths"]
-    assert st["migrated"] == st["resumed"] and st["overflow"] == 0, st  # no path lost in the tail
     return acc, rc, st, px
 
 

@@ -261,41 +261,3 @@ def test_ragged_and_tiny_images(have_gpu, w, h):
     assert st["rays"] == o_cnt["rays"] and st["paths"] == w * h * 5
     assert np.array_equal(acc.view(np.uint32), o_acc.view(np.uint32))
 
-
-TAIL_CASES = [
-    ("cornell_box_original", 128, 128, 1000, 40, {}),                                 # 4-frame sample staging
-    ("cornell_box_volume", 96, 96, 16, 16, {}),                                        # octet staging, 7 waves
-    ("final_render_book_1", 96, 54, 500, 8, {}),                                       # frame tiles, defocus
-    ("book2_final_scene_10000_samples", 64, 64, 10000, 6, {}),                         # media, motion, noise
-    ("cornell_box_original", 1024, 1024, 1000, 24, dict(band_h=2, rank=3, world=8)),  # an 8-way rank
-]
-
-
-@pytest.mark.parametrize("tail", [64, 16])
-@pytest.mark.parametrize("name,w,h,spp,frames,part", TAIL_CASES,
-                         ids=[f"{c[0]}_{c[1]}x{c[2]}" + ("_rank" if c[5] else "") for c in TAIL_CASES])
-def test_tail_compaction_is_invisible(have_gpu, name, w, h, spp, frames, part, tail):
-    """Launch-tail compaction (paths moved between waves through the migrant queue, a drain launch
-    for the rest) gives bit-identical accumulations, pixels and per-pixel ray counts to a render
-    without it, and every moved path is taken up again (migrated == resumed, no overflow). tail 64:
-    every wave with a free lane and nothing to take gives its paths away (most moves)."""
-    base = gpu_render(name, w, h, spp, frames, tail=0, **part)
-    acc, rc, st, px = gpu_render(name, w, h, spp, frames, tail=tail, stats=True, **part)
-    assert st["migrated"] > 0, st
-    assert np.array_equal(acc.view(np.uint32), base[0].view(np.uint32))
-    assert np.array_equal(rc, base[1]) and np.array_equal(px, base[3])
-    assert st["rays"] == base[2]["rays"]
-
-
-def test_tail_compaction_against_oracle(have_gpu, monkeypatch):
-    """Aggressive compaction (tail 64) in the stack traversal and in the threaded one, several
-    launches, against the CPU restatement."""
-    name, w, h, spp, frames = "cornell_box_volume", 72, 40, 64, 13
-    o_acc, o_rc, _ = oracle_render(name, w, h, spp, frames, forward=True)
-    for mode in ("linear", "stack_lds"):
-        for k, v in MODES[mode].items():
-            monkeypatch.setenv(k, v)
-        acc, rc, st, _ = gpu_render(name, w, h, spp, frames, tail=64, launch_frames=5, stats=True)
-        assert st["migrated"] > 0 and st["launches"] == 3
-        np.testing.assert_array_equal(rc, o_rc)
-        assert np.array_equal(acc.view(np.uint32), o_acc.view(np.uint32)), mode

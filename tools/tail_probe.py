@@ -4,7 +4,7 @@ times of one render launch, 100 MHz ticks. Prints, per configuration, the launch
 chip ran after the first wave ran out of work (the tail), and the mean wave time spent after its
 first idle lane.
 
-  RT2_LIB=build/endtime/librt2.so python tools/tail_probe.py [tail]
+  RT2_LIB=raytrace2_amd/lib/ablate/endtime.so python tools/tail_probe.py [ranks]
 """
 import json
 import os
@@ -15,7 +15,7 @@ import torch  # noqa: E402,F401
 import raytrace2_amd as R  # noqa: E402
 
 
-def probe(scene, w, h, spp, band=0, rank=0, world=1, work_split=None, max_depth=50, tail=None):
+def probe(scene, w, h, spp, band=0, rank=0, world=1, work_split=None, max_depth=50):
     sc = R.Scene(os.path.join("scenes", scene), R.DEFAULT_SEED)
     tr = R.RayTracer(sc, 0)
     tr.SetSamplesPerPixel(spp)
@@ -25,8 +25,6 @@ def probe(scene, w, h, spp, band=0, rank=0, world=1, work_split=None, max_depth=
         tr.set_partition(band, rank, world)
     if work_split is not None:
         tr.set_work_split(work_split)
-    if tail is not None:
-        tr.set_tail_compaction(tail)
     tr.Render(spp)
     tr.synchronize()  # warm
     tr.Reset()
@@ -42,17 +40,15 @@ def probe(scene, w, h, spp, band=0, rank=0, world=1, work_split=None, max_depth=
            "span_ms": (t_end - t0) / 1e5, "start_spread_ms": (t0max - t0) / 1e5,
            "first_idle_ms": (idle_min - t0) / 1e5, "last_idle_ms": (idle_max - t0) / 1e5,
            "tail_ms": (t_end - idle_min) / 1e5, "mean_wave_after_idle_ms": idle_sum / max(1, waves) / 1e5,
-           "mean_wave_ms": wave_sum / max(1, waves) / 1e5, "grays_s": st["rays"] / st["kernel_ms"] / 1e6,
-           "tail_min": tail, "migrated": st["migrated"], "resumed": st["resumed"]}
+           "mean_wave_ms": wave_sum / max(1, waves) / 1e5, "grays_s": st["rays"] / st["kernel_ms"] / 1e6}
     tr.close()
     print(json.dumps({k: (round(v, 3) if isinstance(v, float) else v) for k, v in out.items()}), flush=True)
 
 
 if __name__ == "__main__":
-    if len(sys.argv) > 1 and sys.argv[1] == "tail":  # launch-tail compaction thresholds
-        for t in (0, 4, 8, 16, 32):
-            probe("cornell_box_original.json", 1024, 1024, 1000, tail=t)
-            probe("cornell_box_original.json", 1024, 1024, 1000, band=2, rank=0, world=8, tail=t)
+    if len(sys.argv) > 1 and sys.argv[1] == "ranks":  # the headline and its 8-way rank
+        probe("cornell_box_original.json", 1024, 1024, 1000)
+        probe("cornell_box_original.json", 1024, 1024, 1000, band=2, rank=0, world=8)
         sys.exit(0)
     probe("cornell_box_original.json", 1024, 1024, 1000)
     probe("cornell_box_original.json", 1024, 1024, 125)
