@@ -226,9 +226,10 @@ RT2_API int rt2_tracer_get_stats(rt2_tracer* tr, rt2_stats* out);
 RT2_API int rt2_tracer_reset_stats(rt2_tracer* tr);
 
 /* Diagnostic: checks the kernel's exact arithmetic shortcuts against their reference form on n
- * random inputs on `device` (which 0: division by a correctly rounded reciprocal; which 1: the
- * NaN-free slab test; which 2: reciprocal and square root without range scaling). Writes the
- * number of mismatches and of inputs checked. */
+ * random inputs on `device` (which 0: division by a correctly rounded reciprocal, accepted quad
+ * distances; which 1: the NaN-free slab test; which 2: reciprocal and square root without range
+ * scaling; which 3: division by a correctly rounded reciprocal over any quotient, numerators down to
+ * 2^-100). Writes the number of mismatches and of inputs checked. */
 RT2_API int rt2_selftest(int device, int which, uint64_t n, uint64_t seed, uint64_t* mismatches, uint64_t* checked);
 
 /* ---- util::WriteImage (Util.cpp:39-79): sqrt gamma, clamp(x*255.999), vertical flip ---- */

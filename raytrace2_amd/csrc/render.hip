@@ -70,7 +70,7 @@ constexpr int kBlock = 256;
 #define RT2_MIN_WAVES_BOOK1 8
 #endif
 #ifndef RT2_MIN_WAVES_VOL
-#define RT2_MIN_WAVES_VOL 7
+#define RT2_MIN_WAVES_VOL 8  // round 3, with box boundaries as one block: 7 / 8 waves 19.9 k / 20.6 k Mray/s
 #endif
 #ifndef RT2_MIN_WAVES_B2LIN
 #define RT2_MIN_WAVES_B2LIN 8  // book 2 threaded (2000 spp): 6/7/8 waves 1685/1788/1887 Mray/s since its tree steps run in
@@ -927,6 +927,8 @@ __device__ __forceinline__ bool boundary_t_lin(const void* recs, uint32_t ref, f
 // order, each by the unit-normal test with IEEE division: t = (sD - o_K) / d_K is exactly
 // Quad::Hit's (D - n.o) / (n.d) for n = +-e_K (negation commutes with rounding), the interior test is
 // quad_cand_aa's, and the interval test is Contains (inclusive).
+// (div_by_inv with the ray's reciprocal instead of the division: +0.7 % at 7 waves, -0.6 % at 8;
+// not used)
 template <int K>
 __device__ __forceinline__ bool quad_aa_div(const uint32_t* r, f3 o, f3 d, float& t_out) {
   constexpr int A = (K + 1) % 3, B = (K + 2) % 3;
@@ -1612,11 +1614,10 @@ __device__ __forceinline__ uint32_t local_index(const LoopArgs& A, uint32_t xy) 
 }
 
 // Occupancy target (waves per SIMD the register allocation must allow), chosen per variant by
-// measurement (threaded kernels, round 2): Cornell 8 (7: -3 %), Cornell volume 7 (8 with the Philox
-// block in LDS: the same speed, more spill traffic), book 1 8, book 2 7 (6: -3 %; spills VGPRs, but
-// its scalar loads are latency bound), the book 2 /
-// all-features stack kernels 6. Other stack and the counting kernels keep the compiler's own
-// allocation.
+// measurement (threaded kernels): Cornell 8 (7: -3 %), Cornell volume 8 (round 3, with box boundaries
+// as one block: 7 / 8 waves 19.9 k / 20.6 k Mray/s), book 1 8, book 2 8 (6 / 7: -11 / -5 %; spills
+// VGPRs, but its scalar loads are latency bound), the book 2 / all-features stack kernels 6. Other
+// stack and the counting kernels keep the compiler's own allocation.
 template <uint32_t F, int kMode, bool kStats>
 constexpr int MinWaves() {
   if (RT2_MIN_WAVES_PER_EU > 0) return RT2_MIN_WAVES_PER_EU;
@@ -1626,7 +1627,7 @@ constexpr int MinWaves() {
   if (F == kBook2 && !kStats && kMode == kModeLinear) return RT2_MIN_WAVES_B2LIN;
   if (kStats || kMode != kModeLinear) return 1;
   if (F == kFeatXform) return RT2_MIN_WAVES_CORNELL;  // Cornell: 64 VGPRs at 8
-  if (F == (kFeatXform | kFeatMedium)) return RT2_MIN_WAVES_VOL;  // Cornell volume: 72 VGPRs at 7
+  if (F == (kFeatXform | kFeatMedium)) return RT2_MIN_WAVES_VOL;  // Cornell volume
   if (F == kFeatAll) return 1;
   return RT2_MIN_WAVES_BOOK1;                     // book 1
 }
@@ -1639,8 +1640,8 @@ constexpr int MinWaves() {
 // 4/3 of the sample bytes reach memory). Returns the group size, 0 = direct 12-B stores.
 // The threaded product kernels at 8 waves per SIMD keep the Philox block in LDS (PathT; 1 KB per
 // wave): four VGPRs fewer live across the loop, which removed the Cornell kernel's spills at 8
-// waves (12 VGPRs; +1 %). The 7-wave kernels (book 2, Cornell volume) keep it in VGPRs (book 2: -2 % in
-// LDS) and stage whole sample octets instead.
+// waves (12 VGPRs; +1 %). Kernels at 7 waves or fewer keep it in VGPRs and stage whole sample
+// octets instead.
 template <uint32_t F, int kMode, bool kStats>
 constexpr bool LdsRng() {
   return kMode == kModeLinear && !kStats && MinWaves<F, kMode, kStats>() >= 8;
@@ -2119,6 +2120,7 @@ KernelFn Kernel(int v, int mode, bool stats) {
 // ------------------------------------------------------------------------------------------
 // Self-tests of the kernel's exact shortcuts on random inputs (rt2_selftest):
 //   which 0: div_by_inv(a, b, fl(1/b)) == a / b for |b| > 1e-8, |a / b| >= 1e-3 (accepted quad t)
+//   which 3: the same for any quotient with 2^-100 <= |a| < 2^21 (medium box boundaries, any t)
 //   which 1: aabb_hit_fin == aabb_hit for rays with finite inv
 //   which 2: rcp_nr == 1/x and sqrt_nr == sqrt(x) in their ranges
 __device__ __forceinline__ float rand_float(uint32_t bits, int emin, int emax, uint32_t sel) {
@@ -2131,7 +2133,14 @@ __global__ void selftest_kernel(int which, unsigned long long n, uint32_t seed, 
        idx += (unsigned long long)gridDim.x * blockDim.x) {
     uint32_t r0, r1, r2, r3;
     philox(seed, 0x7E57u, (uint32_t)idx, (uint32_t)(idx >> 32), 0u, r0, r1, r2, r3);
-    if (which == 0) {
+    if (which == 3) {
+      const float a = rand_float(r0, -100, 20, r2 & 0xFFFFu);
+      const float b = rand_float(r1, -27, 1, r2 >> 16);
+      const float q = a / b;
+      if (!(fabsf(b) > 1e-8f) || !__builtin_isfinite(q)) continue;
+      checked++;
+      if (__float_as_uint(div_by_inv(a, b, 1.0f / b)) != __float_as_uint(q)) bad++;
+    } else if (which == 0) {
       const float a = rand_float(r0, -30, 17, r2 & 0xFFFFu);
       const float b = rand_float(r1, -27, 1, r2 >> 16);
       const float q = a / b;

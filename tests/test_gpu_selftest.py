@@ -7,14 +7,16 @@
   glm::max/min chain with early exits (AABB.hpp:34-47) for every ray with a finite inverse.
 * rcp_nr / sqrt_nr: 1/x and sqrt(x) without the range-scaling steps equal the IEEE results over
   the ranges where the kernel uses them (normalize, ray reciprocals).
+* div_by_inv over any quotient with numerators down to 2^-100 (a medium box boundary uses every t;
+  the kernel guards smaller numerators back to IEEE division).
 """
 import pytest
 
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("which,n", [(0, 1 << 28), (1, 1 << 26), (2, 1 << 28)],
-                         ids=["div_by_inv", "aabb_fin", "rcp_sqrt_nr"])
+@pytest.mark.parametrize("which,n", [(0, 1 << 28), (1, 1 << 26), (2, 1 << 28), (3, 1 << 28)],
+                         ids=["div_by_inv", "aabb_fin", "rcp_sqrt_nr", "div_by_inv_any_t"])
 def test_selftest(have_gpu, which, n):
     from raytrace2_amd._native import selftest
     bad, checked = selftest(which, n, seed=20241015)
