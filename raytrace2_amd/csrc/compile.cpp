@@ -337,11 +337,11 @@ struct Flattener {
       uint32_t axis;
       memcpy(&axis, &r[11], 4);
       if (axis < 4 || axis > 6) return 0;
-      const int kk = (int)axis - 4;
-      float rec[8];  // QUADAA test words of QUAD (n, D | q, mat | u, axis | v | w, sD)
-      if (!RectAA(r, kk, rec)) return 0;
+      const int kk = (int)axis - 4, a = (kk + 1) % 3, b = (kk + 2) % 3;
+      // (sD, w[K], q[A], q[B], u[A], u[B], v[A], v[B]) of QUAD (n, D | q, mat | u, axis | v | w, sD)
+      const float rec[8] = {r[19], r[16 + kk], r[4 + a], r[4 + b], r[8 + a], r[8 + b], r[12 + a], r[12 + b]};
       words.insert(words.end(), rec, rec + 8);
-      codes |= (uint32_t)kk << (3 * k);
+      codes |= (axis - 4) << (3 * k);
     }
     lind.insert(lind.end(), words.begin(), words.end());
     return kBoundaryAAFlag | ((uint32_t)o.children.size() << 24) | codes;
@@ -426,13 +426,14 @@ struct Flattener {
         uint32_t axis;
         memcpy(&axis, &lind[4 * (off + 2) + 3], 4);
         lind_axis[off] = axis;
-        const float* r = out.nodes.data() + 4 * (size_t)src;
-        float t8[8];
-        if (axis >= 4 && axis <= 6 && !RectAA(r, (int)axis - 4, t8)) lind_axis[off] = axis - 3;  // QUAD layout
-        if (axis >= 4 && axis <= 6 && lind_axis[off] == axis) {  // QUADAA layout (rt2_layout.h)
+        if (axis >= 4 && axis <= 6) {  // QUADAA layout (rt2_layout.h)
+          const int k = (int)axis - 4, a = (k + 1) % 3, b = (k + 2) % 3;
+          const float* r = out.nodes.data() + 4 * (size_t)src;
           const float n[3] = {r[0], r[1], r[2]}, d = r[3], q[3] = {r[4], r[5], r[6]}, mat = r[7];
-          const float rec[20] = {t8[0], t8[1], t8[2], t8[3], t8[4], t8[5], t8[6], t8[7], n[0], n[1],
-                                 n[2],  d,     q[0],  q[1],  q[2],  mat,   Bits(axis), Bits(parent_xf), 0, 0};
+          const float u[3] = {r[8], r[9], r[10]}, v[3] = {r[12], r[13], r[14]}, w[3] = {r[16], r[17], r[18]};
+          const float sd = r[19];
+          const float rec[20] = {sd,   w[k], q[a], q[b], u[a], u[b],        v[a], v[b], n[0], n[1],
+                                 n[2], d,    q[0], q[1], q[2], mat, Bits(axis), Bits(parent_xf), 0, 0};
           std::copy(rec, rec + 20, lind.begin() + 4 * (long)off);
         } else {
           lind[4 * (off + 3) + 3] = Bits(parent_xf);  // enclosing transform of this occurrence

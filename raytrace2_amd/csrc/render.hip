@@ -79,12 +79,6 @@ constexpr int kBlock = 256;
 #ifndef RT2_MIN_WAVES_ALL
 #define RT2_MIN_WAVES_ALL 6
 #endif
-#ifndef RT2_TAIL_MERGE
-#define RT2_TAIL_MERGE 16  // launch-tail merge threshold (paths per departing wave; 0 = off)
-#endif
-#ifndef RT2_QUAD_RECT
-#define RT2_QUAD_RECT 1
-#endif
 #ifndef RT2_ACC_FMA
 #define RT2_ACC_FMA 1
 #endif
@@ -818,26 +812,8 @@ __device__ __forceinline__ bool quad_cand_unit(const float* w, f3 o, f3 d, f3 in
   t_out = t;
   return !(fabsf(dk) <= 1e-8f) && (0.0f <= alpha && alpha <= 1.0f) && (0.0f <= beta && beta <= 1.0f);
 }
-// The interior test of a QUADAA record r = (sD, w[K], q[A], q[B], u[A], 0, 0, v[B]) (a rectangle,
-// rt2_layout.h RectAA) at the plane point's offsets (pva, pvb) from q: Quad::Hit's
-// alpha = w . cross(pv, v) = w[K] (pva v[B] - v[A] pvb) and beta = w . cross(u, pv) =
-// w[K] (u[A] pvb - pva u[B]) without the products of a zero edge component: x - 0 * y is x in
-// value (a signed zero aside, which no comparison below tells apart) whenever y is finite, and
-// when y is not, the other coordinate's test, which keeps y times a nonzero component, rejects in
-// both forms. So the decision is the reference's on every input. (A rectangle with u along B is
-// stored with u and v exchanged and w negated: alpha and beta trade places, the same decision.)
-__device__ __forceinline__ bool quad_inside(const float* r, float pva, float pvb) {
-#if RT2_QUAD_RECT
-  const float alpha = r[1] * (pva * r[7]);
-  const float beta = r[1] * (r[4] * pvb);
-#else
-  const float alpha = r[1] * (pva * r[7] - r[6] * pvb);  // w . cross(pv, v)
-  const float beta = r[1] * (r[4] * pvb - pva * r[5]);   // w . cross(u, pv)
-#endif
-  return (0.0f <= alpha && alpha <= 1.0f) && (0.0f <= beta && beta <= 1.0f);
-}
-// Unit-normal axis-aligned Quad::Hit from a QUADAA record: t as quad_cand_unit, the interior test
-// above.
+// Unit-normal axis-aligned Quad::Hit from a QUADAA record r = (sD, w[K], q[A], q[B], u[A], u[B],
+// v[A], v[B]): the same operations as quad_cand_unit on the same values.
 template <int K>
 __device__ __forceinline__ bool quad_aa(const float* r, f3 o, f3 d, f3 inv, float& t_out) {
   constexpr int A = (K + 1) % 3, B = (K + 2) % 3;
@@ -845,8 +821,10 @@ __device__ __forceinline__ bool quad_aa(const float* r, f3 o, f3 d, f3 inv, floa
   const float t = div_by_inv(r[0] - comp<K>(o), dk, comp<K>(inv));
   const float pva = (comp<A>(o) + comp<A>(d) * t) - r[2];
   const float pvb = (comp<B>(o) + comp<B>(d) * t) - r[3];
+  const float alpha = r[1] * (pva * r[7] - r[6] * pvb);  // w . cross(pv, v)
+  const float beta = r[1] * (r[4] * pvb - pva * r[5]);   // w . cross(u, pv)
   t_out = t;
-  return !(fabsf(dk) <= 1e-8f) && quad_inside(r, pva, pvb);
+  return !(fabsf(dk) <= 1e-8f) && (0.0f <= alpha && alpha <= 1.0f) && (0.0f <= beta && beta <= 1.0f);
 }
 __device__ __forceinline__ bool quad_aa_k(uint32_t k, const float* r, f3 o, f3 d, f3 inv, float& t) {
   if (k == 0u) return quad_aa<0>(r, o, d, inv, t);
@@ -1014,14 +992,16 @@ __device__ __forceinline__ bool boundary_t_lin(const void* recs, uint32_t ref, f
 // (div_by_inv with the ray's reciprocal instead of the division: +0.7 % at 7 waves, -0.6 % at 8;
 // not used)
 template <int K>
-__device__ __forceinline__ bool quad_aa_div(const float* r, f3 o, f3 d, float& t_out) {
+__device__ __forceinline__ bool quad_aa_div(const uint32_t* r, f3 o, f3 d, float& t_out) {
   constexpr int A = (K + 1) % 3, B = (K + 2) % 3;
   const float dk = comp<K>(d);
-  const float t = (r[0] - comp<K>(o)) / dk;
-  const float pva = (comp<A>(o) + comp<A>(d) * t) - r[2];
-  const float pvb = (comp<B>(o) + comp<B>(d) * t) - r[3];
+  const float t = (uf(r[0]) - comp<K>(o)) / dk;
+  const float pva = (comp<A>(o) + comp<A>(d) * t) - uf(r[2]);
+  const float pvb = (comp<B>(o) + comp<B>(d) * t) - uf(r[3]);
+  const float alpha = uf(r[1]) * (pva * uf(r[7]) - uf(r[6]) * pvb);
+  const float beta = uf(r[1]) * (uf(r[4]) * pvb - pva * uf(r[5]));
   t_out = t;
-  return !(fabsf(dk) <= 1e-8f) && quad_inside(r, pva, pvb);
+  return !(fabsf(dk) <= 1e-8f) && (0.0f <= alpha && alpha <= 1.0f) && (0.0f <= beta && beta <= 1.0f);
 }
 // The words come two quads (one 64-byte scalar load) at a time: no dependent loads, few SGPRs.
 __device__ __forceinline__ bool boundary_aa(const void* recs, uint32_t off, uint32_t hdr, f3 o, f3 d, float lo,
@@ -1033,9 +1013,9 @@ __device__ __forceinline__ bool boundary_aa(const void* recs, uint32_t off, uint
 #pragma unroll
     for (uint32_t j = 0; j < 2u; j++) {
       if (k + j < n) {
-        float r[8];
+        uint32_t r[8];
 #pragma unroll
-        for (int i = 0; i < 8; i++) r[i] = uf(w[8 * j + i]);
+        for (int i = 0; i < 8; i++) r[i] = w[8 * j + i];
         const uint32_t code = (hdr >> (3u * (k + j))) & 7u;
         float t;
         bool ok;
@@ -1774,24 +1754,6 @@ constexpr uint32_t StageGroup() {
   return MinWaves<F, kMode, kStats>() <= 7 && !LdsRng<F, kMode, kStats>() ? 8u : 4u;
 }
 
-// Launch-tail merge (threaded product kernels). Once the work items are exhausted, a wave keeps
-// running until its last path ends, issuing whole bounces for the few lanes still live. A wave of
-// the workgroup with at most kTailMerge live paths hands them to a sibling wave that has that many
-// free lanes, through LDS, and exits: the paths continue unchanged (the same state, RNG stream
-// and sample slots), so the results are the same bits. One LDS word per workgroup orders it,
-// changed only by compare-and-swap: live waves (bits 4-7) | waves whose paths wait in their
-// mailbox (bits 0-3). A wave departs only while another is live, leaves only with an empty
-// mailbox set, and the last live wave can neither, so every handed-over path is taken up.
-// A mailbox: word 0 = number of paths, then kMigWords path words in planes of 16 lanes.
-constexpr uint32_t kTailMerge = RT2_TAIL_MERGE;
-static_assert(kTailMerge <= 16, "mailbox planes hold 16 paths");
-constexpr uint32_t kMigWords = 19;  // ro 3, rd 3, thr 3, time, xy, frame, sij, n, dl, Philox block 4
-constexpr uint32_t kMailbox = 1u + 16u * kMigWords;
-template <uint32_t F, int kMode, bool kStats>
-constexpr bool TailMerge() {
-  return kTailMerge > 0 && kMode == kModeLinear && !kStats;
-}
-
 template <uint32_t F, int kMode, bool kStats>
 __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render_kernel(const RenderParams P) {
   constexpr bool kLds = kMode == kModeStackLds || kMode == kModeStackHybrid;
@@ -1805,17 +1767,11 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
   }
   uint32_t* stk = reinterpret_cast<uint32_t*>(s_dyn + (kLds ? P.lds_nodes : 0u)) + threadIdx.x;
   const int lane = (int)__lane_id();
-  constexpr bool kLdsRng = LdsRng<F, kMode, kStats>();
-  constexpr bool kPark = Park<F, kMode, kStats>();
-  constexpr bool kMerge = TailMerge<F, kMode, kStats>();
-  // the waves' LDS planes: sample staging, Philox blocks, park planes, tail-merge mailboxes
-  __shared__ float s_oct[kGroup != 0u ? (kBlock / 64) * kPlanes * 64 : 1];
-  __shared__ uint32_t s_rng[kLdsRng ? (kBlock / 64) * 4 * 64 : 1];
-  __shared__ uint32_t s_park[kPark ? (kBlock / 64) * kParkWords * 64 : 1];
-  __shared__ uint32_t s_mbox[kMerge && !kPark ? (kBlock / 64) * kMailbox : 1];
-  __shared__ uint32_t s_ctl;
   float* oct_wave = nullptr;  // this wave's staging planes (wave-uniform; lanes add their id)
-  if constexpr (kGroup != 0u) oct_wave = s_oct + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * (kPlanes * 64u);
+  if constexpr (kGroup != 0u) {
+    __shared__ float s_oct[(kBlock / 64) * kPlanes * 64];
+    oct_wave = s_oct + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * (kPlanes * 64u);
+  }
   const f3 bg = mk(P.background[0], P.background[1], P.background[2]);
   bool need = true;   // lane wants a work item
   bool idle = false;  // no work left for this lane: it stays in the loop, masked, until the wave ends,
@@ -1823,30 +1779,19 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
   unsigned long long rays = 0;  // rays cast by the wave (popcounts of a ballot at the loop head)
   uint32_t bnext = 0, bend = 0;  // the wave's reserved batch of work items (wave-uniform)
   uint32_t item_rays = 0;
+  constexpr bool kLdsRng = LdsRng<F, kMode, kStats>();
   PathT<kLdsRng> path;
   path.rbw = nullptr;
-  if constexpr (kLdsRng) path.rbw = s_rng + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * 256u;
+  if constexpr (kLdsRng) {
+    __shared__ uint32_t s_rng[(kBlock / 64) * 4 * 64];
+    path.rbw = s_rng + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * 256u;
+  }
+  constexpr bool kPark = Park<F, kMode, kStats>();
   lds_u32* pk = nullptr;  // this lane's park planes (kPark)
   if constexpr (kPark) {
+    __shared__ uint32_t s_park[(kBlock / 64) * kParkWords * 64];
     pk = (lds_u32*)(s_park) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * (kParkWords * 64u) +
          __lane_id();
-  }
-  // tail merge (kTailMerge): the workgroup's merge word and the waves' mailboxes (book 2: its park
-  // planes, free at the loop head), addressed from constants and the wave's own LDS planes only,
-  // so they hold no registers across the loop
-  static_assert(!kMerge || kLdsRng || kGroup != 0u, "the wave index comes from its LDS planes");
-  static_assert(kParkWords * 64u >= kMailbox, "mailbox in the park planes");
-  auto mbox = [&](uint32_t w) -> lds_u32* {
-    if constexpr (kPark) return (lds_u32*)(s_park) + w * (kParkWords * 64u);
-    return (lds_u32*)(s_mbox) + w * kMailbox;
-  };
-  auto wave_index = [&]() -> uint32_t {  // wave-uniform
-    if constexpr (kLdsRng) return (uint32_t)(path.rbw - s_rng) >> 8;
-    return (uint32_t)(oct_wave - s_oct) / (kPlanes * 64u);
-  };
-  if constexpr (kMerge) {
-    if (threadIdx.x == 0) s_ctl = (kBlock / 64u) << 4;
-    __syncthreads();
   }
   path.xy = 0;
   path.start(0);
@@ -1971,109 +1916,7 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
 #if RT2_EXP_ENDTIME
     if (et_idle == 0ull && __ballot(idle) != 0ull) et_idle = __builtin_amdgcn_s_memrealtime();
 #endif
-    bool leave = false;
-    if constexpr (kMerge) {
-      if (__ballot(idle) != 0ull) {  // items exhausted: the launch tail (see kTailMerge)
-        const unsigned long long busym = __ballot(!idle && !need);
-        const uint32_t nbusy = (uint32_t)__popcll(busym);
-        const uint32_t c = __builtin_amdgcn_readfirstlane(*reinterpret_cast<volatile uint32_t*>(&s_ctl));
-        const uint32_t pend = c & 15u, live = c >> 4;
-        const unsigned long long below = (1ull << lane) - 1ull;
-        if (pend != 0u && 64u - nbusy >= kTailMerge) {
-          // take the paths of the lowest waiting mailbox into free lanes
-          const uint32_t b = (uint32_t)__builtin_ctz(pend);
-          uint32_t ok = 0;
-          if (lane == __builtin_amdgcn_readfirstlane(lane)) {
-            uint32_t expect = c;
-            ok = __hip_atomic_compare_exchange_strong(&s_ctl, &expect, c & ~(1u << b), __ATOMIC_ACQ_REL,
-                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          }
-          if (__builtin_amdgcn_readfirstlane(ok)) {
-            const lds_u32* mb = mbox(b);
-            const uint32_t n = mb[0];
-            const uint32_t r = (uint32_t)__popcll(~busym & below);  // rank among the free lanes
-            if ((idle || need) && r < n) {
-              const lds_u32* q = mb + 1u + r;
-              auto w = [&](uint32_t j) { return *reinterpret_cast<const volatile lds_u32*>(q + 16u * j); };
-              ro = mk(uf(w(0)), uf(w(1)), uf(w(2)));
-              rd = mk(uf(w(3)), uf(w(4)), uf(w(5)));
-              thr = mk(uf(w(6)), uf(w(7)), uf(w(8)));
-              rtime = uf(w(9));
-              path.xy = w(10);
-              path.frame = w(11);
-              path.sij = w(12);
-              path.n = w(13);
-              dl = w(14);
-              if constexpr (kLdsRng) {
-#pragma unroll
-                for (uint32_t k = 0; k < 4u; k++) path.rbw[64u * k + (uint32_t)lane] = w(15u + k);
-              } else {
-                path.r0 = w(15);
-                path.r1 = w(16);
-                path.r2 = w(17);
-                path.r3 = w(18);
-              }
-              need = false;
-              idle = false;
-            }
-          }
-        } else if (nbusy == 0u) {
-          // nothing live and no mailbox waiting: leave the workgroup's count of live waves
-          uint32_t ok = 0;
-          if (lane == __builtin_amdgcn_readfirstlane(lane)) {
-            uint32_t expect = c;
-            ok = pend == 0u && __hip_atomic_compare_exchange_strong(&s_ctl, &expect, (live - 1u) << 4, __ATOMIC_ACQ_REL,
-                                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          }
-          leave = __builtin_amdgcn_readfirstlane(ok) != 0u;
-        } else if (nbusy <= kTailMerge && live >= 2u) {
-          // hand the live paths to a sibling: staged samples to memory first (the mailbox may
-          // share nothing with them, but the taker's staging planes do not hold them)
-          const uint32_t wid = wave_index();
-          lds_u32* mb = mbox(wid);
-          if (!idle && !need) {
-            if constexpr (kGroup != 0u) {
-              const LoopArgs A = loop_args();
-              const uint32_t fr = path.frame - (uint32_t)A.frame_begin();
-              const uint32_t slot = fr & (kOctet - 1u), gs = slot & (kGroup - 1u), g0 = slot - gs;
-              const uint32_t first = max(dl >> 27, g0) - g0;
-              float* blk = A.samples() + 3ull * kOctet * ((unsigned long long)(fr / kOctet) * A.local_pixels() +
-                                                         local_index(A, path.xy));
-              const float* oct = oct_wave + __lane_id();
-              for (uint32_t k = first; k < gs; k++) {
-                blk[3u * (g0 + k)] = oct[64u * (3u * k)];
-                blk[3u * (g0 + k) + 1u] = oct[64u * (3u * k + 1u)];
-                blk[3u * (g0 + k) + 2u] = oct[64u * (3u * k + 2u)];
-              }
-              dl = (dl & 0x07FFFFFFu) | (slot << 27);  // the taker stages from the current slot on
-            }
-            lds_u32* q = mb + 1u + (uint32_t)__popcll(busym & below);
-            auto w = [&](uint32_t j, uint32_t v) { *reinterpret_cast<volatile lds_u32*>(q + 16u * j) = v; };
-            w(0, bits(ro.x)), w(1, bits(ro.y)), w(2, bits(ro.z));
-            w(3, bits(rd.x)), w(4, bits(rd.y)), w(5, bits(rd.z));
-            w(6, bits(thr.x)), w(7, bits(thr.y)), w(8, bits(thr.z));
-            w(9, bits(rtime)), w(10, path.xy), w(11, path.frame), w(12, path.sij), w(13, path.n), w(14, dl);
-            if constexpr (kLdsRng) {
-#pragma unroll
-              for (uint32_t k = 0; k < 4u; k++) w(15u + k, path.rbw[64u * k + (uint32_t)lane]);
-            } else {
-              w(15, path.r0), w(16, path.r1), w(17, path.r2), w(18, path.r3);
-            }
-          }
-          uint32_t ok = 0;
-          if (lane == __builtin_amdgcn_readfirstlane(lane)) {
-            *reinterpret_cast<volatile lds_u32*>(mb) = nbusy;
-            uint32_t expect = c;
-            ok = __hip_atomic_compare_exchange_strong(&s_ctl, &expect, ((live - 1u) << 4) | pend | (1u << wid),
-                                                      __ATOMIC_ACQ_REL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          }
-          leave = __builtin_amdgcn_readfirstlane(ok) != 0u;
-        }
-      }
-    } else {
-      leave = __ballot(!idle) == 0ull;
-    }
-    if (leave) break;  // the wave is done (uniform exit)
+    if (__ballot(!idle) == 0ull) break;  // the wave is done (uniform exit)
     rays += (unsigned long long)__popcll(__ballot(!need && (dl & 0xFFFFu) != 0u));  // RayColor casts below
     if (need) continue;
     RT2_STAMP(st_fetch);

@@ -69,14 +69,10 @@ inline constexpr uint32_t make_ref(uint32_t kind, uint32_t off) { return (kind <
 //          axis = k + 1 when n and w are exactly zero off axis k (exact axis-aligned test),
 //          k + 4 when moreover n[k] = s = +-1 exactly (sD = s * D), else 0
 //          In the threaded program's record copy (lind), v.w = the enclosing XFORM's lind ref.
-//  QUADAA: (threaded-program record copy of a rectangle with axis code K + 4)
-//          (sD, w[K], q[A], q[B]) (u[A], 0, 0, v[B]) (n.xyz, D) (q.xyz, material bits)
+//  QUADAA: (threaded-program record copy of a quad with axis code K + 4)
+//          (sD, w[K], q[A], q[B]) (u[A], u[B], v[A], v[B]) (n.xyz, D) (q.xyz, material bits)
 //          (axis bits, xform ref bits, 0, 0), A = (K + 1) % 3, B = (K + 2) % 3: the test reads
-//          the first 8 words only. Only rectangles take it (RectAA): u along A and v along B, or
-//          u along B and v along A, stored with u and v exchanged and w negated (w = n / n.n with
-//          n = u x v, so exchanging u and v negates it exactly, and alpha and beta trade places).
-//          The kernel's interior test drops the zero products (render.hip quad_aa). Other
-//          unit-normal axis-aligned quads keep the QUAD layout with axis code K + 1.
+//          the first 8 words only
 //  SPHERE: (c0.xyz, radius) (displacement.xyz, material bits)
 //  LIST  : (count bits, flags bits, 0, 0) then child refs, 4 per record. flags bit0 = every
 //          child is a QUAD or SPHERE (iterated inline, no stack traffic).
@@ -100,23 +96,6 @@ inline constexpr uint32_t make_ref(uint32_t kind, uint32_t off) { return (kind <
 //  ACCBVH: (min.xyz, near_ref bits) (max.xyz, far_ref bits); near = the child with the smaller
 //          centroids along the node's split axis (kind - kAccBvh); children are ACCBVH or
 //          ACCSPHERE refs (an ACCSPHERE ref points at the child's SPHERE record)
-// The QUADAA test words of a unit-normal axis-aligned quad on axis K from its QUAD record r (20
-// words), or false when it is not a rectangle along A and B.
-inline bool RectAA(const float* r, int K, float* out) {
-  const int a = (K + 1) % 3, b = (K + 2) % 3;
-  const float uA = r[8 + a], uB = r[8 + b], vA = r[12 + a], vB = r[12 + b], wK = r[16 + K];
-  float eA, fB, sw;
-  if (uB == 0.0f && vA == 0.0f && uA != 0.0f && vB != 0.0f) {
-    eA = uA, fB = vB, sw = wK;
-  } else if (uA == 0.0f && vB == 0.0f && uB != 0.0f && vA != 0.0f) {
-    eA = vA, fB = uB, sw = -wK;  // u and v exchanged
-  } else {
-    return false;
-  }
-  const float w[8] = {r[19], sw, r[4 + a], r[4 + b], eA, 0.0f, 0.0f, fB};
-  for (int i = 0; i < 8; i++) out[i] = w[i];
-  return true;
-}
 constexpr uint32_t kListLeafOnly = 1u;
 constexpr uint32_t kBoundaryAAFlag = 0x80000000u;
 constexpr uint32_t kBoundaryAAMax = 6;

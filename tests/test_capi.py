@@ -79,21 +79,3 @@ def test_paired_program_steps_are_well_formed(tmp_path, scene, expect):
     r = subprocess.run([exe, os.path.join(ROOT, "scenes", scene + ".json"), str(expect)], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
     assert r.stdout.startswith("pairs=")
-
-
-@pytest.mark.parametrize("scene", ["cornell_box_original", "cornell_box_volume", "book2_final_scene_10000_samples"])
-def test_rectangle_quad_shortcut_matches_quad_hit(tmp_path, scene):
-    """The threaded kernel's rectangle quads (rt2_layout.h RectAA, render.hip quad_inside: the interior
-    test without the products of zero edge components, u/v exchanged and w negated when u runs along
-    B) decide every ray like Quad::Hit (Quad.cpp:19-43), t included, on random rays and on rays aimed
-    at the quads' edges and corners (host emulation, -ffp-contract=off)."""
-    csrc = os.path.join(ROOT, "raytrace2_amd", "csrc")
-    exe = str(tmp_path / "quad_rect")
-    r = subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
-                        "-I", csrc, "-o", exe, os.path.join(ROOT, "tests", "cpp", "quad_rect.cpp")]
-                       + [os.path.join(csrc, f) for f in ("json.cpp", "scene.cpp", "compile.cpp")],
-                       capture_output=True, text=True)
-    assert r.returncode == 0, r.stderr[-2000:]
-    r = subprocess.run([exe, os.path.join(ROOT, "scenes", scene + ".json"), "20000"], capture_output=True, text=True)
-    assert r.returncode == 0, r.stderr[-2000:]
-    assert r.stdout.startswith("rect=")
