@@ -393,10 +393,12 @@ struct Flattener {
       }
       case kList:
         if (acc_depth.count(i)) {  // LISTACC step (the ray's padding), then its tree in pre-order
-          emit(kListAcc, CopyRecords(src, 2, lind), 0);
+          const size_t me = emit(kListAcc, CopyRecords(src, 2, lind), 0);
           uint32_t root;
           memcpy(&root, &out.nodes[4 * (size_t)src + 7], 4);
-          return LinearizeAcc(root, lin, lind);
+          if (!LinearizeAcc(root, lin, lind)) return false;
+          lin[4 * me + 1] = (uint32_t)(lin.size() / 4);  // skip = the index after the tree
+          return true;
         }
         for (int c : o.children)
           if (!Linearize(c, parent_xf, lin, lind, xf_depth)) return false;

@@ -79,6 +79,9 @@ constexpr int kBlock = 256;
 #ifndef RT2_MIN_WAVES_ALL
 #define RT2_MIN_WAVES_ALL 6
 #endif
+#ifndef RT2_ACC_LANE
+#define RT2_ACC_LANE 1
+#endif
 #ifndef RT2_ACC_FMA
 #define RT2_ACC_FMA 1
 #endif
@@ -1489,6 +1492,54 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
       acc_pad = (uf(aw[8]) * L + uf(aw[9])) * L + uf(aw[10]);
 #endif
       acc_best = kRefNone;
+#if RT2_ACC_LANE
+      // The tree's steps (at + 1 .. skip) walked lane by lane: each lane follows the steps it
+      // would take in the lockstep walk, in the same order (the same tests, the same hit), but the
+      // wave now pays its longest lane's walk instead of the union of its lanes' walks. The steps
+      // come by vector loads of the wide program (64 B per step, the tree is L2-resident).
+      {
+        const uint32_t end = st.y;
+        const uint4* wide = reinterpret_cast<const uint4*>(P.lin_wide);
+        uint32_t j = at + 1u;
+        while (j < end) {
+          // e0 = (kind, skip, after a hit, after a paired miss), e1..e3 = words 4..15
+          const uint4 e0 = wide[4u * j], e1 = wide[4u * j + 1u], e2 = wide[4u * j + 2u], e3 = wide[4u * j + 3u];
+          if (e0.x == kAccBvh) {
+            if (kStats) cnt.bvh++;
+            const float ax = fmaf(uf(e1.x) - o.x, inv.x, -acc_pinv.x), bx = fmaf(uf(e2.x) - o.x, inv.x, acc_pinv.x);
+            const float ay = fmaf(uf(e1.y) - o.y, inv.y, -acc_pinv.y), by = fmaf(uf(e2.y) - o.y, inv.y, acc_pinv.y);
+            const float az = fmaf(uf(e1.z) - o.z, inv.z, -acc_pinv.z), bz = fmaf(uf(e2.z) - o.z, inv.z, acc_pinv.z);
+            float t0, t1;
+            slab_t(ax, bx, ay, by, az, bz, tmin, tmax, t0, t1);
+            const bool in = t0 <= t1;
+            uint32_t nx = in ? j + 1u : e0.y;
+            if (e0.z != j + 1u) {  // paired with its near child (words 7, 11-15)
+              const float cx = fmaf(uf(e1.w) - o.x, inv.x, -acc_pinv.x), dx = fmaf(uf(e3.y) - o.x, inv.x, acc_pinv.x);
+              const float cy = fmaf(uf(e2.w) - o.y, inv.y, -acc_pinv.y), dy = fmaf(uf(e3.z) - o.y, inv.y, acc_pinv.y);
+              const float cz = fmaf(uf(e3.x) - o.z, inv.z, -acc_pinv.z), dz = fmaf(uf(e3.w) - o.z, inv.z, acc_pinv.z);
+              float u0, u1;
+              slab_t(cx, dx, cy, dy, cz, dz, tmin, tmax, u0, u1);
+              if (kStats && in) cnt.bvh++;
+              nx = in ? (u0 <= u1 ? e0.z : e0.w) : e0.y;
+            }
+            j = nx;
+          } else {  // ACCSPHERE: the record's words inline, aux = list position
+            if (kStats) cnt.sphere++;
+            float t;
+            if (sphere_t_rec(make_float4(uf(e1.x), uf(e1.y), uf(e1.z), uf(e1.w)),
+                             make_float4(uf(e2.x), uf(e2.y), uf(e2.z), uf(e2.w)), o, d, time, tmin, FLT_MAX, t) &&
+                (t < tmax || (t == tmax && acc_best != kRefNone && e0.w < acc_best))) {
+              tmax = t;
+              prim = make_ref(kSphere, e0.z);
+              h.xf = cur_xf;
+              acc_best = e0.w;
+            }
+            j++;
+          }
+        }
+        next = end;
+      }
+#endif
     } else if (Has<F, kFeatAccList>() && kind == kAccSphere) {
       const u32x16& aw = sw;
       // smallest root wins; an equal root goes to the lower child index (aux = the child's
