@@ -79,12 +79,6 @@ constexpr int kBlock = 256;
 #ifndef RT2_MIN_WAVES_ALL
 #define RT2_MIN_WAVES_ALL 6
 #endif
-#ifndef RT2_ACC_LANE
-#define RT2_ACC_LANE 1
-#endif
-#ifndef RT2_ACC_FMA
-#define RT2_ACC_FMA 1
-#endif
 #ifndef RT2_PARK
 #define RT2_PARK 1
 #endif
@@ -1277,11 +1271,7 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
   float tmax = FLT_MAX;
   uint32_t prim = kRefNone;  // closest primitive so far (h.xf: its transform, quads: from the record)
   uint32_t cur_xf = kRefNone;
-#if RT2_ACC_FMA
   f3 acc_pinv = mk(0.0f, 0.0f, 0.0f);  // accelerated list: this ray's box padding x inv
-#else
-  float acc_pad = 0.0f;          // accelerated list: this ray's box padding
-#endif
   uint32_t acc_best = kRefNone;  // accelerated list: child index of its current closest sphere
   uint32_t next = 0;  // this lane's next step
   const uint32_t len = P.lin_len;
@@ -1292,56 +1282,18 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
   uint32_t i = wave_min_next(next);  // wave-uniform step = min over live lanes of `next`
   while (i < len) {
     u32x16 sw = sld16(P.lin_wide, i * 64u);  // entry + the first 48 bytes of its record
-#define RT2_IS_RUN(k) ((k) == kBvh || (Has<F, kFeatAccList>() && (k) == kAccBvh))
-    if (RT2_IS_RUN(sw[0])) {
-      // A run of BVH steps (scene BVH and accelerated-list trees) in a loop of their own: only
-      // `next` changes from step to step, so nothing else is carried (no register copies between
-      // kinds) and the step costs the slab test, the next-index update and the wave-minimum search.
-      // A paired step (compile.cpp: word 2 is not i + 1; sphere scenes only) also tests its near
-      // child's box (words 7, 11-15), with the tmax that child's own step would see (nothing runs
-      // between the two in pre-order), and jumps past it.
+    if (sw[0] == kBvh) {
+      // A run of BVH steps in a loop of their own: only `next` changes from step to step, so
+      // nothing else is carried (no register copies between kinds) and the step costs the slab
+      // test, the next-index update and the wave-minimum search. A paired step (compile.cpp: word
+      // 2 is not i + 1; sphere scenes only) also tests its near child's box (words 7, 11-15), with
+      // the tmax that child's own step would see (nothing runs between the two in pre-order), and
+      // jumps past it. (Accelerated-list trees are walked lane by lane at their LISTACC step.)
       const bool allfin = __all(fin);
       do {
         RT2_WAVE(1);
         RT2_WAVE(2);
-        if (Has<F, kFeatAccList>() && sw[0] == kAccBvh) {
-          if (next == i) {  // padded slab test of an accelerated list's tree node
-            if (kStats) cnt.bvh++;
-#if RT2_ACC_FMA
-            // (lo - pad - o) inv = (lo - o) inv - pad inv as one fma: the tree is this library's
-            // conservative cull (the pad exceeds these roundings by orders of magnitude), not the
-            // reference's, so it need not round like AABB::Hit; an infinite inv gives NaN slabs,
-            // which the min/max ignore (no cull on that axis)
-            const float ax = fmaf(uf(sw[4]) - o.x, inv.x, -acc_pinv.x), bx = fmaf(uf(sw[8]) - o.x, inv.x, acc_pinv.x);
-            const float ay = fmaf(uf(sw[5]) - o.y, inv.y, -acc_pinv.y), by = fmaf(uf(sw[9]) - o.y, inv.y, acc_pinv.y);
-            const float az = fmaf(uf(sw[6]) - o.z, inv.z, -acc_pinv.z), bz = fmaf(uf(sw[10]) - o.z, inv.z, acc_pinv.z);
-#else
-            const float ax = ((uf(sw[4]) - acc_pad) - o.x) * inv.x, bx = ((uf(sw[8]) + acc_pad) - o.x) * inv.x;
-            const float ay = ((uf(sw[5]) - acc_pad) - o.y) * inv.y, by = ((uf(sw[9]) + acc_pad) - o.y) * inv.y;
-            const float az = ((uf(sw[6]) - acc_pad) - o.z) * inv.z, bz = ((uf(sw[10]) + acc_pad) - o.z) * inv.z;
-#endif
-            float t0, t1;
-            slab_t(ax, bx, ay, by, az, bz, tmin, tmax, t0, t1);
-            const bool in = t0 <= t1;
-            uint32_t nx = in ? i + 1u : sw[1];
-            if (sw[2] != i + 1u) {  // paired with its near child's step, same tmax and padding
-#if RT2_ACC_FMA
-              const float cx = fmaf(uf(sw[7]) - o.x, inv.x, -acc_pinv.x), dx = fmaf(uf(sw[13]) - o.x, inv.x, acc_pinv.x);
-              const float cy = fmaf(uf(sw[11]) - o.y, inv.y, -acc_pinv.y), dy = fmaf(uf(sw[14]) - o.y, inv.y, acc_pinv.y);
-              const float cz = fmaf(uf(sw[12]) - o.z, inv.z, -acc_pinv.z), dz = fmaf(uf(sw[15]) - o.z, inv.z, acc_pinv.z);
-#else
-              const float cx = ((uf(sw[7]) - acc_pad) - o.x) * inv.x, dx = ((uf(sw[13]) + acc_pad) - o.x) * inv.x;
-              const float cy = ((uf(sw[11]) - acc_pad) - o.y) * inv.y, dy = ((uf(sw[14]) + acc_pad) - o.y) * inv.y;
-              const float cz = ((uf(sw[12]) - acc_pad) - o.z) * inv.z, dz = ((uf(sw[15]) + acc_pad) - o.z) * inv.z;
-#endif
-              float u0, u1;
-              slab_t(cx, dx, cy, dy, cz, dz, tmin, tmax, u0, u1);
-              if (kStats && in) cnt.bvh++;
-              nx = in ? (u0 <= u1 ? sw[2] : sw[3]) : sw[1];
-            }
-            next = nx;
-          }
-        } else if (next == i) {
+        if (next == i) {
           if (kStats) cnt.bvh++;
           const float4 lo = make_float4(uf(sw[4]), uf(sw[5]), uf(sw[6]), 0.0f);
           const float4 hi = make_float4(uf(sw[8]), uf(sw[9]), uf(sw[10]), 0.0f);
@@ -1368,16 +1320,15 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
         i = wave_min_next(next);
         if (i >= len) break;
         sw = sld16(P.lin_wide, i * 64u);
-      } while (RT2_IS_RUN(sw[0]));
+      } while (sw[0] == kBvh);
       if (i >= len) break;
     }
-#undef RT2_IS_RUN
     const u32x4 st = {sw[0], sw[1], sw[2], sw[3]};
     const uint32_t kind = st.x, off = st.z;
     RT2_WAVE(1);
     if (kind == kQuad) RT2_WAVE(3);
     if (is_acc_bvh(kind)) RT2_WAVE(2);
-    if (kind == kSphere || kind == kAccSphere) RT2_WAVE(4);
+    if (kind == kSphere) RT2_WAVE(4);
     if (kind == kMedium) RT2_WAVE(5);
     const uint32_t at = i;
     i = kRefNone;  // computed after the step
@@ -1486,17 +1437,14 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
       if (kStats) cnt.list++;
       const f3 dc = o - mk(uf(aw[4]), uf(aw[5]), uf(aw[6]));
       const float L = sqrtf(dot(dc, dc)) * 1.0001f + uf(aw[7]);
-#if RT2_ACC_FMA
       acc_pinv = ((uf(aw[8]) * L + uf(aw[9])) * L + uf(aw[10])) * inv;  // inv: the list's space
-#else
-      acc_pad = (uf(aw[8]) * L + uf(aw[9])) * L + uf(aw[10]);
-#endif
       acc_best = kRefNone;
-#if RT2_ACC_LANE
-      // The tree's steps (at + 1 .. skip) walked lane by lane: each lane follows the steps it
-      // would take in the lockstep walk, in the same order (the same tests, the same hit), but the
-      // wave now pays its longest lane's walk instead of the union of its lanes' walks. The steps
-      // come by vector loads of the wide program (64 B per step, the tree is L2-resident).
+      // The tree's steps (at + 1 .. skip) are walked lane by lane: each lane follows its own
+      // pre-order path (skip on a miss, paired child boxes), the steps a lockstep walk would have
+      // taken for it, in the same order (the same tests, the same hit), so the wave pays its
+      // longest lane's walk instead of the union of its lanes' walks (rays enter the list from
+      // every direction: book 2 +30 %). Steps come by vector loads of the wide program (64 B each;
+      // the tree is L2-resident).
       {
         const uint32_t end = st.y;
         const uint4* wide = reinterpret_cast<const uint4*>(P.lin_wide);
@@ -1538,21 +1486,6 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
           }
         }
         next = end;
-      }
-#endif
-    } else if (Has<F, kFeatAccList>() && kind == kAccSphere) {
-      const u32x16& aw = sw;
-      // smallest root wins; an equal root goes to the lower child index (aux = the child's
-      // record offset in the node array, which is list order)
-      if (kStats) cnt.sphere++;
-      float t;
-      if (sphere_t_rec(make_float4(uf(aw[4]), uf(aw[5]), uf(aw[6]), uf(aw[7])),
-                       make_float4(uf(aw[8]), uf(aw[9]), uf(aw[10]), uf(aw[11])), o, d, time, tmin, FLT_MAX, t) &&
-          (t < tmax || (t == tmax && acc_best != kRefNone && st.w < acc_best))) {
-        tmax = t;
-        prim = make_ref(kSphere, off);
-        h.xf = cur_xf;
-        acc_best = st.w;
       }
     } else if (Has<F, kFeatMedium>() && kind == kMedium) {
       if (kStats) cnt.medium++;
