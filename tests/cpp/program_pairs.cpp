@@ -64,7 +64,23 @@ int main(int argc, char** argv) {
     for (int j = 0; j < 6; j++)
       if (std::memcmp(&w[words[j]], &b[rec[j]], 4) != 0) return fail("child box words", i);
   }
-  std::printf("pairs=%zu steps=%zu\n", pairs, n);
+  // LISTACC steps: skip = the index after the list's tree, whose steps (and only they) lie between
+  // (the kernel walks them lane by lane, render.hip)
+  size_t lists = 0;
+  for (size_t i = 0; i < n; i++) {
+    if (c.lin[4 * i] != kListAcc) continue;
+    lists++;
+    const size_t end = c.lin[4 * i + 1];
+    if (end <= i + 1 || end > n) return fail("LISTACC skip is not past its tree", i);
+    for (size_t j = i + 1; j < end; j++)
+      if (c.lin[4 * j] != kAccBvh && c.lin[4 * j] != kAccSphere) return fail("a non-tree step inside a LISTACC tree", j);
+    if (end < n && (c.lin[4 * end] == kAccBvh || c.lin[4 * end] == kAccSphere)) return fail("LISTACC skip lands in a tree", i);
+    for (size_t j = i + 1; j < end; j++)
+      if (c.lin[4 * j] == kAccBvh && (c.lin[4 * j + 1] <= j || c.lin[4 * j + 1] > end || c.lin_wide[16 * j + 2] > end ||
+                                       c.lin_wide[16 * j + 3] > end))
+        return fail("a tree step's targets leave the tree", j);
+  }
+  std::printf("pairs=%zu steps=%zu lists=%zu\n", pairs, n, lists);
   const bool expect = std::atoi(argv[2]) != 0;
   if (expect != (pairs > 0)) return fail(expect ? "no pairs" : "unexpected pairs", 0);
   return 0;
