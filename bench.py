@@ -51,11 +51,19 @@ KERNEL_SOURCES = ["raytrace2_amd/csrc/render.hip", "raytrace2_amd/csrc/rt2_layou
 
 
 def kernel_sha() -> str:
-    """Identity of the render kernel build: a profile only describes the source it was taken on."""
+    """Identity of the render kernel sources in this tree: a profile only describes the build it was
+    taken on."""
     h = hashlib.sha1()
     for f in KERNEL_SOURCES:
         h.update(open(os.path.join(ROOT, f), "rb").read())
     return h.hexdigest()[:12]
+
+
+def library_kernel_sha(R) -> str:
+    """The kernel sha the loaded librt2.so was built from (rt2_version's last field; the Makefile
+    embeds it), which is what actually ran."""
+    v = R.lib.rt2_version().decode(errors="replace").split()
+    return v[-1] if len(v) >= 2 and v[-2] == "kernel" else "unknown"
 
 
 def parse():
@@ -328,7 +336,11 @@ def main():
         partition = f"{n_gpus}-way h={a.band_h} rank 0"
     else:
         partition = "1 GPU"
-    key = {"workload": workload, "partition": partition, "kernel_sha": kernel_sha()}
+    lib_sha, src_sha = library_kernel_sha(R), kernel_sha()
+    if lib_sha != src_sha:  # a library built from other sources than this tree's: key on what ran
+        print(f"bench.py: librt2.so was built from kernel sources {lib_sha}, this tree has {src_sha}",
+              file=sys.stderr)
+    key = {"workload": workload, "partition": partition, "kernel_sha": lib_sha}
     roofline = None
     cpu = None
     if rank == 0:
@@ -384,7 +396,7 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "detail": {"rays": int(rays_total), "launches": me["launches"], "setup_s": round(setup_s, 3),
-                       "kernel_sha": key["kernel_sha"],
+                       "kernel_sha": key["kernel_sha"], "source_kernel_sha": src_sha,
                        "kernel_ms_per_step_max": round(max(r["kernel_ms"] for r in per_rank) / a.steps, 2),
                        "gather_ms_per_step": round(per_rank[0]["gather_ms"] / a.steps, 3),
                        "per_rank": [{"rank": r["rank"], "rows": r["rows"], "mray_s": round(r["mray_s"], 1),

@@ -36,6 +36,8 @@ typedef struct rt2_scene rt2_scene;
 typedef struct rt2_tracer rt2_tracer;
 
 RT2_API const char* rt2_last_error(void);
+/* "rt2-mi355x <version> (gfx950) kernel <12 hex digits>": the last field identifies the kernel sources
+ * (render.hip + rt2_layout.h) the library was built from */
 RT2_API const char* rt2_version(void);
 
 /* ---- SceneLoader::LoadScene (Serialize.cpp:199-360) + App.cpp:126 (top-level BVHNode) ----

@@ -297,7 +297,11 @@ void Put3(float* d, vec3 v) {
 extern "C" {
 
 const char* rt2_last_error(void) { return g_err.c_str(); }
-const char* rt2_version(void) { return "rt2-mi355x 0.1 (gfx950)"; }
+#ifndef RT2_KERNEL_SHA
+#define RT2_KERNEL_SHA "unknown"
+#endif
+// "rt2-mi355x 0.1 (gfx950) kernel <sha1 of render.hip + rt2_layout.h, 12 hex digits>"
+const char* rt2_version(void) { return "rt2-mi355x 0.1 (gfx950) kernel " RT2_KERNEL_SHA; }
 
 int rt2_scene_load(const char* path, uint64_t seed, rt2_scene** out) {
   if (!path || !out) return Fail(RT2_ERR_INVALID, "rt2_scene_load: null argument");
