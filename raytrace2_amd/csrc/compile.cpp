@@ -349,7 +349,9 @@ struct Flattener {
   // An accelerated list's tree in the threaded program: ACCBVH steps (padded box, skip = index
   // after the subtree) near child first, ACCSPHERE steps with aux = the sphere's record offset in
   // the node array, which is the list's child order (the kernel breaks equal roots by it).
-  bool LinearizeAcc(uint32_t ref, std::vector<uint32_t>& lin, std::vector<float>& lind) {
+  // `octant` (bit k: the ray direction is negative along axis k) orders each node's children for
+  // such rays: the child with the larger centroids first along a split axis the ray runs down.
+  bool LinearizeAcc(uint32_t ref, std::vector<uint32_t>& lin, std::vector<float>& lind, uint32_t octant = 0) {
     if (lin.size() / 4 >= LinearMaxSteps()) return false;
     const uint32_t kind = ref >> 28, off = ref & kOffsetMask;
     if (kind == kAccSphere) {
@@ -361,7 +363,8 @@ struct Flattener {
     uint32_t near_ref, far_ref;
     memcpy(&near_ref, &out.nodes[4 * (size_t)off + 3], 4);
     memcpy(&far_ref, &out.nodes[4 * (size_t)off + 7], 4);
-    if (!LinearizeAcc(near_ref, lin, lind) || !LinearizeAcc(far_ref, lin, lind)) return false;
+    if ((octant >> (kind - kAccBvh)) & 1u) std::swap(near_ref, far_ref);
+    if (!LinearizeAcc(near_ref, lin, lind, octant) || !LinearizeAcc(far_ref, lin, lind, octant)) return false;
     lin[4 * me + 1] = (uint32_t)(lin.size() / 4);
     return true;
   }
@@ -393,11 +396,22 @@ struct Flattener {
       }
       case kList:
         if (acc_depth.count(i)) {  // LISTACC step (the ray's padding), then its tree in pre-order
+          // LISTACC step (aux = steps per copy of the tree, skip = the index after the copies), then
+          // the tree in pre-order, and, when they fit, seven more copies, one per ray-direction
+          // octant, each visiting a node's children nearer-first for rays of that octant (the list's
+          // answer does not depend on the order: rt2_layout.h LISTACC). RT2_ACC_OCTANTS=0: one copy.
           const size_t me = emit(kListAcc, CopyRecords(src, 2, lind), 0);
           uint32_t root;
           memcpy(&root, &out.nodes[4 * (size_t)src + 7], 4);
+          const size_t first = lin.size() / 4;
           if (!LinearizeAcc(root, lin, lind)) return false;
-          lin[4 * me + 1] = (uint32_t)(lin.size() / 4);  // skip = the index after the tree
+          const uint32_t copy = (uint32_t)(lin.size() / 4 - first);
+          lin[4 * me + 3] = copy;
+          const char* oe = getenv("RT2_ACC_OCTANTS");
+          if (!(oe && atoi(oe) == 0) && lin.size() / 4 + 7 * (size_t)copy <= LinearMaxSteps())
+            for (uint32_t oct = 1; oct < 8; oct++)
+              if (!LinearizeAcc(root, lin, lind, oct)) return false;
+          lin[4 * me + 1] = (uint32_t)(lin.size() / 4);
           return true;
         }
         for (int c : o.children)

@@ -1449,7 +1449,10 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
         const uint32_t end = st.y;
         const uint4* wide = reinterpret_cast<const uint4*>(P.lin_wide);
         uint32_t j = at + 1u;
-        while (j < end) {
+        // eight copies of the tree (compile.cpp): the one ordered nearer-first for this ray's octant
+        if (end - j > st.w) j += st.w * ((d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u));
+        const uint32_t stop = j + st.w;
+        while (j < stop) {
           // e0 = (kind, skip, after a hit, after a paired miss), e1..e3 = words 4..15
           const uint4 e0 = wide[4u * j], e1 = wide[4u * j + 1u], e2 = wide[4u * j + 2u], e3 = wide[4u * j + 3u];
           if (e0.x == kAccBvh) {

@@ -144,8 +144,10 @@ constexpr int kLdsSceneBytesMax = 96 * 1024;  // scenes up to this size are stag
 //   kind kXform: enter the transform (record = XFORM record, skip = index of its kXformExit);
 //     the kernel walks the steps up to the exit in a nested loop with the transformed ray
 //   kind kXformExit: leave it (record = XFORM record, aux = parent XFORM ref or kRefNone)
-//   kind kListAcc: an accelerated list (record = LISTACC, skip = index after its tree): sets the
-//     ray's box padding; its tree follows in pre-order, near child first: kind kAccBvh (record = ACCBVH, skip = index after
+//   kind kListAcc: an accelerated list (record = LISTACC, skip = index after its tree's copies,
+//     aux = steps per copy): sets the ray's box padding; its tree follows in pre-order (one copy,
+//     or eight: copy k visits a node's children nearer-first for rays whose direction is negative
+//     along the axes of k's bits), near child first: kind kAccBvh (record = ACCBVH, skip = index after
 //     the subtree, padded box test) and kind kAccSphere (record = SPHERE, aux = the sphere's
 //     record offset in the node array, i.e. its list position, for the equal-root rule)
 // Lists vanish (their children follow each other); span-1 leaves with a medium appear twice.

@@ -70,8 +70,9 @@ int main(int argc, char** argv) {
   for (size_t i = 0; i < n; i++) {
     if (c.lin[4 * i] != kListAcc) continue;
     lists++;
-    const size_t end = c.lin[4 * i + 1];
+    const size_t end = c.lin[4 * i + 1], copy = c.lin[4 * i + 3];
     if (end <= i + 1 || end > n) return fail("LISTACC skip is not past its tree", i);
+    if (copy == 0 || (end - i - 1 != copy && end - i - 1 != 8 * copy)) return fail("LISTACC copies", i);
     for (size_t j = i + 1; j < end; j++)
       if (c.lin[4 * j] != kAccBvh && c.lin[4 * j] != kAccSphere) return fail("a non-tree step inside a LISTACC tree", j);
     if (end < n && (c.lin[4 * end] == kAccBvh || c.lin[4 * end] == kAccSphere)) return fail("LISTACC skip lands in a tree", i);
