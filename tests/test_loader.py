@@ -52,7 +52,8 @@ def test_scene_compile_facts():
     assert b2.spheres == 1007 and b2.xforms == 1 and b2.media == 2 and b2.quads == 400 * 6 + 1
     # the 1000-sphere list under the transform gets an exact acceleration tree (n - 1 nodes), threaded
     # into the program after its LISTACC step: 1 + 999 + 1000 of the program's 4922 steps
-    assert (b2.acc_lists, b2.acc_nodes, b2.linear_steps) == (1, 999, 4922)
+    # the list's tree (999 nodes + 1000 spheres = 1999 steps) in eight octant-ordered copies
+    assert (b2.acc_lists, b2.acc_nodes, b2.linear_steps) == (1, 999, 4922 + 7 * 1999)
     assert b2.max_stack <= 24
     assert info.acc_lists == 0 and info.linear_steps > 0
 
