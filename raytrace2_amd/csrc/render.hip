@@ -79,6 +79,9 @@ constexpr int kBlock = 256;
 #ifndef RT2_MIN_WAVES_ALL
 #define RT2_MIN_WAVES_ALL 6
 #endif
+#ifndef RT2_BOX_PAIR
+#define RT2_BOX_PAIR 1
+#endif
 #ifndef RT2_PARK
 #define RT2_PARK 1
 #endif
@@ -1035,6 +1038,57 @@ __device__ __forceinline__ bool boundary_aa(const void* recs, uint32_t off, uint
   return any;
 }
 
+// Both boundary queries of ConstantMedium::Hit (ConstantMedium.cpp:14-58) on a box in one pass:
+// each quad's t and interior decision do not depend on the query's interval, so its quads are
+// tested once and the two answers selected from the candidates — t1 = the smallest candidate in
+// [-FLT_MAX, FLT_MAX] (Interval::universe, kInfinity = FLT_MAX), t2 = the smallest in
+// [fl(t1 + 0.0001), FLT_MAX] — which is what the two HittableList queries return (the closest hit in
+// the interval; only its t is used). Half the quad tests of the two queries.
+__device__ __forceinline__ bool boundary_aa_pair(const void* recs, uint32_t off, uint32_t hdr, f3 o, f3 d, float& t1,
+                                                 float& t2, Counters& cnt) {
+  const uint32_t n = (hdr >> 24) & 7u;
+  float c[kBoundaryAAMax];  // candidate t, +inf when the quad is missed (no interval accepts it)
+#pragma unroll
+  for (uint32_t k = 0; k < kBoundaryAAMax; k += 2u) {
+    c[k] = c[k + 1u] = INFINITY;
+    if (k < n) {  // wave-uniform
+      const u32x16 w = sld16(recs, off + 32u * k);
+#pragma unroll
+      for (uint32_t j = 0; j < 2u; j++) {
+        if (k + j < n) {
+          uint32_t r[8];
+#pragma unroll
+          for (int i = 0; i < 8; i++) r[i] = w[8 * j + i];
+          const uint32_t code = (hdr >> (3u * (k + j))) & 7u;
+          float t;
+          bool ok;
+          if (code == 0u) {
+            ok = quad_aa_div<0>(r, o, d, t);
+          } else if (code == 1u) {
+            ok = quad_aa_div<1>(r, o, d, t);
+          } else {
+            ok = quad_aa_div<2>(r, o, d, t);
+          }
+          cnt.quad += 2;  // the two queries' tests
+          if (ok && -FLT_MAX <= t && t <= FLT_MAX) c[k + j] = t;
+        }
+      }
+    }
+  }
+  float m = c[0];
+#pragma unroll
+  for (uint32_t k = 1; k < kBoundaryAAMax; k++) m = fminf(m, c[k]);
+  if (!(m <= FLT_MAX)) return false;
+  t1 = m;
+  const float lb = (float)((double)m + 0.0001);
+  float m2 = INFINITY;
+#pragma unroll
+  for (uint32_t k = 0; k < kBoundaryAAMax; k++) m2 = (lb <= c[k] && c[k] < m2) ? c[k] : m2;
+  if (!(m2 <= FLT_MAX)) return false;
+  t2 = m2;
+  return true;
+}
+
 // medium_t with the boundary queries above (same operations, same random draw)
 template <uint32_t F, class G>
 __device__ __forceinline__ bool medium_t_lin(const void* recs, uint32_t moff, const u32x4 r0, f3 o, f3 d, float time,
@@ -1044,8 +1098,12 @@ __device__ __forceinline__ bool medium_t_lin(const void* recs, uint32_t moff, co
   // a box (the sphere scenes' kernels keep the general path: the 48 words cost them SGPRs)
   if (!Has<F, kFeatSphere>() && (r0.w & kBoundaryAAFlag)) {
     const uint32_t off = (moff + 1u) * 16u;
+#if RT2_BOX_PAIR
+    if (!boundary_aa_pair(recs, off, r0.w, o, d, t1, t2, cnt)) return false;
+#else
     if (!boundary_aa(recs, off, r0.w, o, d, -FLT_MAX, FLT_MAX, t1, cnt)) return false;
     if (!boundary_aa(recs, off, r0.w, o, d, (float)((double)t1 + 0.0001), FLT_MAX, t2, cnt)) return false;
+#endif
   } else {
 #if RT2_EXP_TWICE & 128
   {
