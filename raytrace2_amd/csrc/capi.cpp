@@ -60,6 +60,7 @@ struct rt2_tracer {
   uint32_t node_records = 0;
   uint32_t features = 0;
   int max_stack = 1;
+  bool stack_ok = true;  // the scene fits the stack traversal (else only the threaded program runs it)
   bool use_lds = true;
   bool use_hybrid = true;   // stage only the BVH prefix in LDS when the scene is too large
   bool force_hybrid = false;  // tests: hybrid even when the whole scene would fit
@@ -518,6 +519,7 @@ int rt2_tracer_create(const rt2_scene* s, int device, rt2_tracer** out) {
   t->hot_records = c.hot_records;
   t->features = c.features;
   t->max_stack = c.max_stack;
+  t->stack_ok = c.stack_ok;
   Put3(t->background, s->scene.background);
   t->camera = s->scene.cam;
   HIP_TRY(hipDeviceGetAttribute(&t->cus, hipDeviceAttributeMultiprocessorCount, device));
@@ -706,6 +708,8 @@ int rt2_tracer_last_launch(const rt2_tracer* t, int* grid, int* chunk_frames, in
 int rt2_tracer_on_resize(rt2_tracer* t, int w, int h) {
   if (!t || w <= 0 || h <= 0) return Fail(RT2_ERR_INVALID, "dims must be positive");
   if (w > 65535 || h > 65535) return Fail(RT2_ERR_INVALID, "dims must be at most 65535");
+  // the kernel's pixel index (Philox pixel word, magic division by the width) stays below 2^31
+  if ((int64_t)w * h >= (int64_t)1 << 31) return Fail(RT2_ERR_INVALID, "width * height must be below 2^31");
   if (IsMulti(t)) {
     t->width = w;
     t->height = h;
@@ -919,6 +923,10 @@ int LaunchFrames(rt2_tracer* t, int n_frames) {
   p.lin_wide = t->d_lin_wide;
   p.lind = t->d_lind;
   p.lin_len = t->use_linear ? t->lin_len : 0u;
+  if (!p.lin_len && !t->stack_ok)
+    return Fail(RT2_ERR_INVALID, "scene needs a traversal stack of " + std::to_string(t->max_stack) +
+                                     " entries (kernel has " + std::to_string(kTraversalStack) +
+                                     "): only the threaded traversal can render it");
   // Frame tiles (a wave's lanes trace one pixel's consecutive frames: paths from one pixel share
   // their first hit and start their secondary rays from nearly one point, so the lockstep walk of
   // a deep program serves more lanes per step) for deep threaded programs: measured with chunks of
@@ -1026,11 +1034,11 @@ int LaunchFrames(rt2_tracer* t, int n_frames) {
     p.n_frames = L.n_frames;
     p.chunks = t->d_chunks + L.table;
     p.n_chunks = L.n_chunks;
+    p.div_width = MakeMagic((uint32_t)t->width);  // pixel index -> (x, y)
     if (t->frame_tiles) {
       p.frame_tiles = 1u;
       p.frame_tile = 64u * p.local_pixels;
       p.div_frame_tile = MakeMagic(p.frame_tile);
-      p.div_width = MakeMagic((uint32_t)t->width);
       p.n_items = (L.n_chunks / 64u) * p.frame_tile;
     } else {
       p.n_items = L.n_chunks * p.tile_items;
@@ -1551,7 +1559,7 @@ int rt2_tracer_image_pixels(rt2_tracer* t, uint8_t* out) {
 
 int rt2_selftest(int device, int which, uint64_t n, uint64_t seed, uint64_t* mismatches, uint64_t* checked) {
   if (!mismatches || !checked) return Fail(RT2_ERR_INVALID, "null argument");
-  if (which < 0 || which > 3) return Fail(RT2_ERR_INVALID, "unknown self-test");
+  if (which < 0 || which > 4) return Fail(RT2_ERR_INVALID, "unknown self-test");
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return Fail(RT2_ERR_HIP, "no HIP device available");
   HIP_TRY(hipSetDevice(device));

@@ -22,6 +22,9 @@ struct Flattener {
   std::unordered_map<int, int> acc_depth;    // accelerated list obj -> tree depth
   std::unordered_map<uint32_t, uint32_t> lind_axis;  // program quad record -> axis code
   bool accelerate_lists = true;
+  // depth of an accelerated list's tree beyond the balanced ceil(log2 n) that SAH splits may use
+  // (CompileScene retries with 0 when the scene's traversal stack would not fit)
+  int acc_depth_slack = kAccDepthSlack;
   std::unordered_map<int, bool> medium_memo;
 
   Flattener(const Scene& sc, CompiledScene& o) : s(sc), out(o) {}
@@ -80,8 +83,11 @@ struct Flattener {
     return true;
   }
   // Binary tree over the children's boxes (SAH split, or the median on the longest centroid axis);
-  // returns the subtree ref and its depth.
-  uint32_t BuildAcc(std::vector<std::pair<int, uint32_t>>& items, size_t lo, size_t hi, int& depth) {
+  // returns the subtree ref and its depth, at most `budget`: a split leaves each side at most
+  // 2^(budget - 1) children, which the median split always does when hi - lo <= 2^budget, so
+  // the SAH cannot build the lopsided (up to n - 1 levels deep) trees that clustered or graded
+  // sphere sizes invite.
+  uint32_t BuildAcc(std::vector<std::pair<int, uint32_t>>& items, size_t lo, size_t hi, int budget, int& depth) {
     if (hi - lo == 1) {
       depth = 0;
       return make_ref(kAccSphere, items[lo].second & kOffsetMask);
@@ -119,6 +125,7 @@ struct Flattener {
       };
       double best = 1e300;
       const size_t n = hi - lo;
+      const size_t side_max = budget - 1 >= 62 ? n : std::min(n, (size_t)1 << (budget - 1));
       std::vector<float> right(n);
       for (int ax = 0; ax < 3; ax++) {
         std::sort(items.begin() + (long)lo, items.begin() + (long)hi, less_on(ax));
@@ -130,6 +137,7 @@ struct Flattener {
         acc = s.objs[(size_t)items[lo].first].aabb;
         for (size_t k = 1; k < n; k++) {  // left = [lo, lo + k)
           acc = AABB(acc, s.objs[(size_t)items[lo + k - 1].first].aabb);
+          if (k > side_max || n - k > side_max) continue;  // a side deeper than the budget allows
           const double c = (double)area(acc) * (double)k + (double)right[k] * (double)(n - k);
           if (c < best) best = c, axis = ax, mid = lo + k;
         }
@@ -137,8 +145,8 @@ struct Flattener {
     }
     std::sort(items.begin() + (long)lo, items.begin() + (long)hi, less_on(axis));
     int dl = 0, dr = 0;
-    uint32_t l = BuildAcc(items, lo, mid, dl);
-    uint32_t r = BuildAcc(items, mid, hi, dr);
+    uint32_t l = BuildAcc(items, lo, mid, budget - 1, dl);
+    uint32_t r = BuildAcc(items, mid, hi, budget - 1, dr);
     depth = 1 + std::max(dl, dr);
     uint32_t off = Alloc(kBvhRecords);
     Put(off, box.x.min, box.y.min, box.z.min, Bits(l));
@@ -156,8 +164,9 @@ struct Flattener {
       rmin = std::min(rmin, c.radius);
       box = AABB(box, c.aabb);
     }
-    int depth = 0;
-    uint32_t root = BuildAcc(items, 0, items.size(), depth);
+    int depth = 0, balanced = 0;
+    while (((size_t)1 << balanced) < items.size()) balanced++;  // ceil(log2 n): the median tree's depth
+    uint32_t root = BuildAcc(items, 0, items.size(), balanced + acc_depth_slack, depth);
     acc_depth[i] = depth;
     vec3 c((box.x.min + box.x.max) * 0.5f, (box.y.min + box.y.max) * 0.5f, (box.z.min + box.z.max) * 0.5f);
     float hx = box.x.max - c.x, hy = box.y.max - c.y, hz = box.z.max - c.z;
@@ -580,6 +589,11 @@ void PackTextures(const Scene& s, CompiledScene& out) {
 }  // namespace
 
 bool CompileScene(const Scene& s, CompiledScene& out, std::string& err, bool accelerate_lists) {
+  return CompileSceneWith(s, out, err, accelerate_lists, kAccDepthSlack);
+}
+
+bool CompileSceneWith(const Scene& s, CompiledScene& out, std::string& err, bool accelerate_lists,
+                      int acc_depth_slack) {
   out = CompiledScene();
   if (s.root < 0) {
     err = "scene has no BVH root";
@@ -614,6 +628,7 @@ bool CompileScene(const Scene& s, CompiledScene& out, std::string& err, bool acc
   out.nodes.assign(4 * (size_t)hot, 0.0f);
   Flattener fl(s, out);
   fl.accelerate_lists = accelerate_lists;
+  fl.acc_depth_slack = acc_depth_slack;
   fl.bvh_rank = &rank;
   out.root = fl.Emit(s.root, kRefNone, err);
   if (out.root == kRefNone) return false;
@@ -624,10 +639,10 @@ bool CompileScene(const Scene& s, CompiledScene& out, std::string& err, bool acc
   int depth = 0;
   out.max_stack = std::max(1, fl.StackNeed(s.root, depth));
   out.bvh_depth = depth;
-  if (out.max_stack > kTraversalStack) {
-    err = "scene needs a traversal stack of " + std::to_string(out.max_stack) + " entries (kernel has " +
-          std::to_string(kTraversalStack) + ")";
-    return false;
+  if (out.max_stack > kTraversalStack && out.acc_lists > 0 && acc_depth_slack > 0) {
+    // the SAH's extra tree depth pushed the stack past the kernel's: balanced trees instead (a
+    // performance heuristic never makes a scene fail to load)
+    return CompileSceneWith(s, out, err, accelerate_lists, 0);
   }
   if (out.nodes.size() / 4 > kOffsetMask) {
     err = "scene too large for 28-bit node offsets";
@@ -636,6 +651,14 @@ bool CompileScene(const Scene& s, CompiledScene& out, std::string& err, bool acc
   if (!fl.Linearize(s.root, kRefNone, out.lin, out.lind)) {
     out.lin.clear();
     out.lind.clear();
+  }
+  // The stack traversal needs max_stack entries per lane; the threaded program needs none, so a
+  // deeper scene still loads when it has one (and then always runs threaded).
+  out.stack_ok = out.max_stack <= kTraversalStack;
+  if (!out.stack_ok && out.lin.empty()) {
+    err = "scene needs a traversal stack of " + std::to_string(out.max_stack) + " entries (kernel has " +
+          std::to_string(kTraversalStack) + ") and has no threaded program";
+    return false;
   }
   // Quad runs: for a quad step, aux = number of consecutive quad steps starting there with no
   // skip target inside the run (so every lane that reaches the run's first step walks all of it).

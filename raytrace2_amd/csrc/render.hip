@@ -85,6 +85,9 @@ constexpr int kBlock = 256;
 #ifndef RT2_PARK
 #define RT2_PARK 1
 #endif
+#ifndef RT2_KEEP_WINV
+#define RT2_KEEP_WINV 1
+#endif
 #ifndef RT2_MIN_WAVES_PER_EU
 #define RT2_MIN_WAVES_PER_EU 0  // 0: per-variant occupancy targets (kMinWaves below)
 #endif
@@ -350,13 +353,10 @@ __device__ __forceinline__ ShadeArgs shade_args() {
 }
 
 
-// Philox keys and the image width (the stream's pixel index), one wait.
-__device__ __forceinline__ void seed_args(uint32_t& k0, uint32_t& k1, uint32_t& width) {
+// Philox keys, one scalar load.
+__device__ __forceinline__ void seed_args(uint32_t& k0, uint32_t& k1) {
   static_assert(RT2_KOFF(seed_hi) == RT2_KOFF(seed_lo) + 4, "RenderParams layout");
-  unsigned long long k;
-  asm volatile("s_load_dwordx2 %0, %2, %3\n\ts_load_dword %1, %2, %4\n\ts_waitcnt lgkmcnt(0)"
-               : "=&s"(k), "=&s"(width)
-               : "s"(__builtin_amdgcn_kernarg_segment_ptr()), "n"(RT2_KOFF(seed_lo)), "n"(RT2_KOFF(width)));
+  const unsigned long long k = karg2<RT2_KOFF(seed_lo)>();
   k0 = (uint32_t)k;
   k1 = (uint32_t)(k >> 32);
 }
@@ -400,26 +400,34 @@ __device__ __forceinline__ uint32_t sel4(uint32_t i, uint32_t r0, uint32_t r1, u
 }
 __device__ __forceinline__ float to_unit(uint32_t v) { return (float)(v >> 8) * (1.0f / 16777216.0f); }
 
+// Per-lane LDS planes: word k of a lane at p[64 k] (p = the wave's plane block + the lane id), so a
+// wave's access to one plane is one conflict-free ds_read / ds_write. The render kernel gives every
+// wave one block of planes (render_kernel: Philox block, sample staging, box-boundary candidates,
+// parked path state) and keeps one per-lane address for all of them: the planes differ by
+// immediate offsets.
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) float lds_f32;
+
 // The per-lane path context the samplers need. kLdsRng: the lane's current Philox block lives in
-// LDS planes (word k of the lane at rbw[64 k + lane]; rbw is the wave's base, wave-uniform) instead
-// of four VGPRs that stay live across the whole render loop.
+// four LDS planes (word k at rb[64 k]) instead of four VGPRs that stay live across the whole render
+// loop.
 template <bool kLdsRng>
 struct PathT {
   static constexpr bool kLds = kLdsRng;
   uint32_t frame;
-  uint32_t xy;   // pixel x | y << 16 (global image coordinates)
+  uint32_t pix;  // global pixel index y * width + x (the stream's pixel word)
   uint32_t sij;  // stratum s_i | s_j << 16 of `frame` (RayTracer.cpp:59-60), advanced per frame
   uint32_t n;
   uint32_t r0, r1, r2, r3;  // the block (kLdsRng false)
-  uint32_t* rbw;            // the wave's LDS planes (kLdsRng true)
+  lds_u32* rb;              // the lane's Philox planes (kLdsRng true)
   __device__ __forceinline__ void start(uint32_t f) {
     frame = f;
     n = 0;  // buffer holds block -1: the first group refills
   }
   __device__ __forceinline__ void block(uint32_t b, uint32_t& w0, uint32_t& w1, uint32_t& w2, uint32_t& w3) const {
-    uint32_t key0, key1, w;
-    seed_args(key0, key1, w);  // re-read at the refill (see karg16)
-    philox(key0, key1, (xy >> 16) * w + (xy & 0xFFFFu), frame, b, w0, w1, w2, w3);
+    uint32_t key0, key1;
+    seed_args(key0, key1);  // re-read at the refill (see karg16)
+    philox(key0, key1, pix, frame, b, w0, w1, w2, w3);
   }
   // K consecutive uniforms in [0,1) (24-bit mantissa), in stream order
   template <int K>
@@ -428,7 +436,6 @@ struct PathT {
     bool fresh = i == 0u;
     uint32_t v[K];
     if constexpr (kLdsRng) {
-      uint32_t* rb = rbw + __lane_id();
 #pragma unroll
       for (int j = 0; j < K; j++) v[j] = rb[64u * ((i + (uint32_t)j) & 3u)];
       if (fresh || i + (uint32_t)K > 4u) {
@@ -469,9 +476,8 @@ struct PathT {
 // the medium step's free-flight draw: it reads the stream position from the planes and writes the
 // advanced count back. Volatile accesses: neither hoisted into registers nor forwarded from the
 // stores.
-enum ParkWord : uint32_t { kPkThr = 0, kPkDl = 3, kPkSij = 4, kPkFrame = 5, kPkXy = 6, kPkN = 7, kPkO = 8,
+enum ParkWord : uint32_t { kPkThr = 0, kPkDl = 3, kPkSij = 4, kPkFrame = 5, kPkPix = 6, kPkN = 7, kPkO = 8,
                            kPkD = 11, kParkWords = 14 };
-typedef __attribute__((address_space(3))) uint32_t lds_u32;  // ds_read / ds_write with offsets
 __device__ __forceinline__ void pk_st(lds_u32* pk, uint32_t w, uint32_t v) {
   *reinterpret_cast<volatile lds_u32*>(pk + 64u * w) = v;
 }
@@ -488,14 +494,14 @@ __device__ __forceinline__ f3 pk_ld3(const lds_u32* pk, uint32_t w) {
 }
 struct ParkedPath {
   static constexpr bool kLds = true;
-  uint32_t* rbw;  // the wave's Philox planes (PathT<true>)
+  lds_u32* rb;  // the lane's Philox planes (PathT<true>)
   lds_u32* pk;    // this lane's park planes
   template <int K>
   __device__ __forceinline__ void take(float* out) {
     PathT<true> p;
-    p.rbw = rbw;
+    p.rb = rb;
     p.frame = pk_ld(pk, kPkFrame);
-    p.xy = pk_ld(pk, kPkXy);
+    p.pix = pk_ld(pk, kPkPix);
     p.n = pk_ld(pk, kPkN);
     p.template take<K>(out);
     pk_st(pk, kPkN, p.n);
@@ -681,6 +687,18 @@ __device__ __forceinline__ bool aabb_hit_fin(float4 lo, float4 hi, f3 o, f3 inv,
   float t0, t1;
   slab_t(ax, bx, ay, by, az, bz, tmin, tmax, t0, t1);
   return !(t1 <= t0);  // AABB::Hit: a miss when t1 <= t0 (AABB.hpp)
+}
+// The padded box test of an accelerated list's tree (the library's own conservative cull, not the
+// reference's AABB::Hit): bounds lo - pad, hi + pad as fma(bound - o, inv, -+pinv) with pinv = pad * inv
+// computed once per ray (inv from acc_slab_inv, rt2_layout.h). rt2_selftest which 4 checks on the
+// GPU that it never rejects a box the ray's exact (double-precision) padded slab accepts.
+__device__ __forceinline__ bool acc_slab(f3 lo, f3 hi, f3 o, f3 inv, f3 pinv, float tmin, float tmax) {
+  const float ax = fmaf(lo.x - o.x, inv.x, -pinv.x), bx = fmaf(hi.x - o.x, inv.x, pinv.x);
+  const float ay = fmaf(lo.y - o.y, inv.y, -pinv.y), by = fmaf(hi.y - o.y, inv.y, pinv.y);
+  const float az = fmaf(lo.z - o.z, inv.z, -pinv.z), bz = fmaf(hi.z - o.z, inv.z, pinv.z);
+  float t0, t1;
+  slab_t(ax, bx, ay, by, az, bz, tmin, tmax, t0, t1);
+  return t0 <= t1;
 }
 __device__ __forceinline__ bool finite3(f3 v) {
   return __builtin_isfinite(v.x) && __builtin_isfinite(v.y) && __builtin_isfinite(v.z);
@@ -1044,46 +1062,46 @@ __device__ __forceinline__ bool boundary_aa(const void* recs, uint32_t off, uint
 // [-FLT_MAX, FLT_MAX] (Interval::universe, kInfinity = FLT_MAX), t2 = the smallest in
 // [fl(t1 + 0.0001), FLT_MAX] — which is what the two HittableList queries return (the closest hit in
 // the interval; only its t is used). Half the quad tests of the two queries.
+// The candidates wait in LDS planes of the wave (word k of the lane at cand[64 k]) between the two
+// selections: held in six VGPRs they pushed the 8-wave kernel into 25 spilled VGPRs (round 3: 56 B
+// of scratch per lane, 32 HBM bytes per ray); only the running minimum stays in a register.
 __device__ __forceinline__ bool boundary_aa_pair(const void* recs, uint32_t off, uint32_t hdr, f3 o, f3 d, float& t1,
-                                                 float& t2, Counters& cnt) {
+                                                 float& t2, lds_u32* cand, Counters& cnt) {
   const uint32_t n = (hdr >> 24) & 7u;
-  float c[kBoundaryAAMax];  // candidate t, +inf when the quad is missed (no interval accepts it)
+  float m = INFINITY;  // candidate t, +inf when the quad is missed (no interval accepts it)
+  for (uint32_t k = 0; k < n; k += 2u) {  // wave-uniform
+    const u32x16 w = sld16(recs, off + 32u * k);
 #pragma unroll
-  for (uint32_t k = 0; k < kBoundaryAAMax; k += 2u) {
-    c[k] = c[k + 1u] = INFINITY;
-    if (k < n) {  // wave-uniform
-      const u32x16 w = sld16(recs, off + 32u * k);
+    for (uint32_t j = 0; j < 2u; j++) {
+      if (k + j < n) {
+        uint32_t r[8];
 #pragma unroll
-      for (uint32_t j = 0; j < 2u; j++) {
-        if (k + j < n) {
-          uint32_t r[8];
-#pragma unroll
-          for (int i = 0; i < 8; i++) r[i] = w[8 * j + i];
-          const uint32_t code = (hdr >> (3u * (k + j))) & 7u;
-          float t;
-          bool ok;
-          if (code == 0u) {
-            ok = quad_aa_div<0>(r, o, d, t);
-          } else if (code == 1u) {
-            ok = quad_aa_div<1>(r, o, d, t);
-          } else {
-            ok = quad_aa_div<2>(r, o, d, t);
-          }
-          cnt.quad += 2;  // the two queries' tests
-          if (ok && -FLT_MAX <= t && t <= FLT_MAX) c[k + j] = t;
+        for (int i = 0; i < 8; i++) r[i] = w[8 * j + i];
+        const uint32_t code = (hdr >> (3u * (k + j))) & 7u;
+        float t;
+        bool ok;
+        if (code == 0u) {
+          ok = quad_aa_div<0>(r, o, d, t);
+        } else if (code == 1u) {
+          ok = quad_aa_div<1>(r, o, d, t);
+        } else {
+          ok = quad_aa_div<2>(r, o, d, t);
         }
+        cnt.quad += 2;  // the two queries' tests
+        const float c = (ok && -FLT_MAX <= t && t <= FLT_MAX) ? t : INFINITY;
+        m = fminf(m, c);
+        pk_st(cand, k + j, bits(c));
       }
     }
   }
-  float m = c[0];
-#pragma unroll
-  for (uint32_t k = 1; k < kBoundaryAAMax; k++) m = fminf(m, c[k]);
   if (!(m <= FLT_MAX)) return false;
   t1 = m;
   const float lb = (float)((double)m + 0.0001);
   float m2 = INFINITY;
-#pragma unroll
-  for (uint32_t k = 0; k < kBoundaryAAMax; k++) m2 = (lb <= c[k] && c[k] < m2) ? c[k] : m2;
+  for (uint32_t k = 0; k < n; k++) {
+    const float c = uf(pk_ld(cand, k));
+    m2 = (lb <= c && c < m2) ? c : m2;
+  }
   if (!(m2 <= FLT_MAX)) return false;
   t2 = m2;
   return true;
@@ -1092,14 +1110,15 @@ __device__ __forceinline__ bool boundary_aa_pair(const void* recs, uint32_t off,
 // medium_t with the boundary queries above (same operations, same random draw)
 template <uint32_t F, class G>
 __device__ __forceinline__ bool medium_t_lin(const void* recs, uint32_t moff, const u32x4 r0, f3 o, f3 d, float time,
-                                             float tmin, float tmax, G& path, float& t_out, Counters& cnt) {
+                                             float tmin, float tmax, G& path, lds_u32* cand, float& t_out,
+                                             Counters& cnt) {
   const uint32_t bref = r0.z;
   float t1, t2;
   // a box (the sphere scenes' kernels keep the general path: the 48 words cost them SGPRs)
   if (!Has<F, kFeatSphere>() && (r0.w & kBoundaryAAFlag)) {
     const uint32_t off = (moff + 1u) * 16u;
 #if RT2_BOX_PAIR
-    if (!boundary_aa_pair(recs, off, r0.w, o, d, t1, t2, cnt)) return false;
+    if (!boundary_aa_pair(recs, off, r0.w, o, d, t1, t2, cand, cnt)) return false;
 #else
     if (!boundary_aa(recs, off, r0.w, o, d, -FLT_MAX, FLT_MAX, t1, cnt)) return false;
     if (!boundary_aa(recs, off, r0.w, o, d, (float)((double)t1 + 0.0001), FLT_MAX, t2, cnt)) return false;
@@ -1315,16 +1334,17 @@ __device__ __forceinline__ uint32_t wave_min_next(uint32_t next) {
 
 template <uint32_t F, bool kStats, class W, class G>
 __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wray, float time, G& path, HitRef& h,
-                                             Counters& cnt) {
+                                             lds_u32* cand, Counters& cnt) {
   const Nodes<kModeLinear> N{reinterpret_cast<const float4*>(P.lind)};  // boundaries / nested xforms
   const void* recs = P.lind;
-  // a parked world ray (ParkRay) is read back where it is needed again, its reciprocal recomputed
-  constexpr bool kKeepW = !__is_same(W, ParkRay);
+  // the world ray's reciprocal is recomputed where a transform's exit returns to world space
+  // (RT2_KEEP_WINV keeps it in registers: three VGPRs live across the whole trace)
+  constexpr bool kKeepW = RT2_KEEP_WINV && !__is_same(W, ParkRay);
   f3 o = wray.wo(), d = wray.wd();
-  const f3 winv = recip3(d);
-  f3 inv = winv;
-  const bool wfin = finite3(winv);
-  bool fin = wfin;  // inv finite: the NaN-free slab test applies
+  f3 inv = recip3(d);
+  const f3 winv = inv;
+  bool fin = finite3(inv);  // inv finite: the NaN-free slab test applies
+  const bool wfin = fin;
   const float tmin = 0.001f;
   float tmax = FLT_MAX;
   uint32_t prim = kRefNone;  // closest primitive so far (h.xf: its transform, quads: from the record)
@@ -1495,6 +1515,12 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
       if (kStats) cnt.list++;
       const f3 dc = o - mk(uf(aw[4]), uf(aw[5]), uf(aw[6]));
       const float L = sqrtf(dot(dc, dc)) * 1.0001f + uf(aw[7]);
+      // The walk's padded slab bound is fma(bound - o, inv, -+pad inv), one rounding per bound. An
+      // infinite inv (a direction component exactly 0) would give NaN or -inf there and cull a box
+      // the ray passes inside the padding; the walk takes +-2^100 for it instead (acc_slab_inv,
+      // rt2_layout.h: conservative), and the exact inv is restored after the walk.
+      const bool clamp = !__all(fin);  // wave-uniform, rare
+      if (clamp) inv = mk(acc_slab_inv(inv.x), acc_slab_inv(inv.y), acc_slab_inv(inv.z));
       acc_pinv = ((uf(aw[8]) * L + uf(aw[9])) * L + uf(aw[10])) * inv;  // inv: the list's space
       acc_best = kRefNone;
       // The tree's steps (at + 1 .. skip) are walked lane by lane: each lane follows its own
@@ -1515,21 +1541,14 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
           const uint4 e0 = wide[4u * j], e1 = wide[4u * j + 1u], e2 = wide[4u * j + 2u], e3 = wide[4u * j + 3u];
           if (e0.x == kAccBvh) {
             if (kStats) cnt.bvh++;
-            const float ax = fmaf(uf(e1.x) - o.x, inv.x, -acc_pinv.x), bx = fmaf(uf(e2.x) - o.x, inv.x, acc_pinv.x);
-            const float ay = fmaf(uf(e1.y) - o.y, inv.y, -acc_pinv.y), by = fmaf(uf(e2.y) - o.y, inv.y, acc_pinv.y);
-            const float az = fmaf(uf(e1.z) - o.z, inv.z, -acc_pinv.z), bz = fmaf(uf(e2.z) - o.z, inv.z, acc_pinv.z);
-            float t0, t1;
-            slab_t(ax, bx, ay, by, az, bz, tmin, tmax, t0, t1);
-            const bool in = t0 <= t1;
+            const bool in = acc_slab(mk(uf(e1.x), uf(e1.y), uf(e1.z)), mk(uf(e2.x), uf(e2.y), uf(e2.z)), o, inv,
+                                     acc_pinv, tmin, tmax);
             uint32_t nx = in ? j + 1u : e0.y;
             if (e0.z != j + 1u) {  // paired with its near child (words 7, 11-15)
-              const float cx = fmaf(uf(e1.w) - o.x, inv.x, -acc_pinv.x), dx = fmaf(uf(e3.y) - o.x, inv.x, acc_pinv.x);
-              const float cy = fmaf(uf(e2.w) - o.y, inv.y, -acc_pinv.y), dy = fmaf(uf(e3.z) - o.y, inv.y, acc_pinv.y);
-              const float cz = fmaf(uf(e3.x) - o.z, inv.z, -acc_pinv.z), dz = fmaf(uf(e3.w) - o.z, inv.z, acc_pinv.z);
-              float u0, u1;
-              slab_t(cx, dx, cy, dy, cz, dz, tmin, tmax, u0, u1);
+              const bool in2 = acc_slab(mk(uf(e1.w), uf(e2.w), uf(e3.x)), mk(uf(e3.y), uf(e3.z), uf(e3.w)), o, inv,
+                                        acc_pinv, tmin, tmax);
               if (kStats && in) cnt.bvh++;
-              nx = in ? (u0 <= u1 ? e0.z : e0.w) : e0.y;
+              nx = in ? (in2 ? e0.z : e0.w) : e0.y;
             }
             j = nx;
           } else {  // ACCSPHERE: the record's words inline, aux = list position
@@ -1547,6 +1566,7 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
           }
         }
         next = end;
+        if (clamp) inv = recip3(d);
       }
     } else if (Has<F, kFeatMedium>() && kind == kMedium) {
       if (kStats) cnt.medium++;
@@ -1559,11 +1579,11 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
         G p2 = path;
         Counters c2 = cnt;
         float t2 = 0.0f;
-        const bool h2 = medium_t_lin<F>(recs, off, mr, o2, d, time, tmin, tmax, p2, t2, c2);
+        const bool h2 = medium_t_lin<F>(recs, off, mr, o2, d, time, tmin, tmax, p2, cand, t2, c2);
         asm volatile("" ::"v"(t2), "v"((int)h2));
       }
 #endif
-      if (medium_t_lin<F>(recs, off, mr, o, d, time, tmin, tmax, path, t, cnt)) {
+      if (medium_t_lin<F>(recs, off, mr, o, d, time, tmin, tmax, path, cand, t, cnt)) {
         tmax = t;
         prim = make_ref(kMedium, off);
         h.xf = cur_xf;
@@ -1694,10 +1714,11 @@ __device__ __forceinline__ f3 tex_value(const ShadeArgs& S, uint32_t idx, f3 p) 
 }
 
 // ------------------------------------------------------------------------------------------
+// Camera::GetRay for global pixel (x, y) at the path's stratum
 template <uint32_t F, class G>
-__device__ __forceinline__ void camera_ray(const RenderParams& P, G& g, f3& o, f3& d, float& time) {
+__device__ __forceinline__ void camera_ray(const RenderParams& P, G& g, uint32_t x, uint32_t y, f3& o, f3& d,
+                                           float& time) {
   const CameraParams& C = P.cam;
-  const int x = (int)(g.xy & 0xFFFFu), y = (int)(g.xy >> 16);
   const int s_i = (int)(g.sij & 0xFFFFu), s_j = (int)(g.sij >> 16);
   float u[3];
   bool defocus = Has<F, kFeatDefocus>() && !(C.defocus_angle <= 0.0f);
@@ -1738,16 +1759,19 @@ __device__ __forceinline__ void camera_ray(const RenderParams& P, G& g, f3& o, f
   d = normalize(pc - c);
 }
 
-// Local (row-band) pixel index of global pixel xy: global row y lies in band y / band_h of period
+// Global pixel index -> (x, y) by the host's multiplier for the width (rt2_layout.h Magic; the
+// index is below 2^31, capi.cpp OnResize)
+__device__ __forceinline__ void pix_xy(const LoopArgs& A, uint32_t pix, uint32_t& x, uint32_t& y) {
+  const unsigned long long dw = karg2<RT2_KOFF(div_width)>();
+  y = udiv(pix, Magic{(uint32_t)dw, (uint32_t)(dw >> 32)});
+  x = pix - y * (uint32_t)A.width();
+}
+// Local (row-band) pixel index of global pixel (x, y): global row y lies in band y / band_h of period
 // y / (band_h * world) and is stored as local row (y / (band_h * world)) * band_h + y % band_h
-// (rt2_layout.h BandRank).
-__device__ __forceinline__ uint32_t local_index(const LoopArgs& A, uint32_t xy) {
-  const uint32_t x = xy & 0xFFFFu, y = xy >> 16;
-  uint32_t r = y;
-  if (A.world() > 1) {
-    const uint32_t bh = (uint32_t)A.band_h();
-    r = udiv(y, A.div_band_w()) * bh + (y - udiv(y, A.div_band_h()) * bh);
-  }
+// (rt2_layout.h BandRank). One GPU: the global index.
+__device__ __forceinline__ uint32_t local_index(const LoopArgs& A, uint32_t x, uint32_t y) {
+  const uint32_t bh = (uint32_t)A.band_h();
+  const uint32_t r = udiv(y, A.div_band_w()) * bh + (y - udiv(y, A.div_band_h()) * bh);
   return r * (uint32_t)A.width() + x;
 }
 
@@ -1799,6 +1823,13 @@ constexpr uint32_t StageGroup() {
   return MinWaves<F, kMode, kStats>() <= 7 && !LdsRng<F, kMode, kStats>() ? 8u : 4u;
 }
 
+// Kernels whose threaded medium step takes both box-boundary queries in one pass (boundary_aa_pair):
+// their LDS holds the candidates.
+template <uint32_t F, int kMode>
+constexpr bool BoxPair() {
+  return RT2_BOX_PAIR && kMode == kModeLinear && Has<F, kFeatMedium>() && !Has<F, kFeatSphere>();
+}
+
 template <uint32_t F, int kMode, bool kStats>
 __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render_kernel(const RenderParams P) {
   constexpr bool kLds = kMode == kModeStackLds || kMode == kModeStackHybrid;
@@ -1812,10 +1843,16 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
   }
   uint32_t* stk = reinterpret_cast<uint32_t*>(s_dyn + (kLds ? P.lds_nodes : 0u)) + threadIdx.x;
   const int lane = (int)__lane_id();
-  float* oct_wave = nullptr;  // this wave's staging planes (wave-uniform; lanes add their id)
-  if constexpr (kGroup != 0u) {
-    __shared__ float s_oct[(kBlock / 64) * kPlanes * 64];
-    oct_wave = s_oct + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * (kPlanes * 64u);
+  constexpr bool kLdsRng = LdsRng<F, kMode, kStats>();
+  constexpr bool kPark = Park<F, kMode, kStats>();
+  // the wave's LDS planes (lds_u32): Philox block, sample staging, box-boundary candidates, parked path
+  constexpr uint32_t kRngP = 0u, kOctP = kRngP + (kLdsRng ? 4u : 0u), kCandP = kOctP + (kGroup ? kPlanes : 0u);
+  constexpr uint32_t kParkP = kCandP + (BoxPair<F, kMode>() ? kBoundaryAAMax : 0u);
+  constexpr uint32_t kWavePlanes = kParkP + (kPark ? (uint32_t)kParkWords : 0u);
+  lds_u32* lp = nullptr;  // this lane's word of plane 0
+  if constexpr (kWavePlanes != 0u) {
+    __shared__ uint32_t s_planes[(kBlock / 64) * kWavePlanes * 64];
+    lp = (lds_u32*)(s_planes) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * (kWavePlanes * 64u) + lane;
   }
   const f3 bg = mk(P.background[0], P.background[1], P.background[2]);
   bool need = true;   // lane wants a work item
@@ -1824,21 +1861,10 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
   unsigned long long rays = 0;  // rays cast by the wave (popcounts of a ballot at the loop head)
   uint32_t bnext = 0, bend = 0;  // the wave's reserved batch of work items (wave-uniform)
   uint32_t item_rays = 0;
-  constexpr bool kLdsRng = LdsRng<F, kMode, kStats>();
   PathT<kLdsRng> path;
-  path.rbw = nullptr;
-  if constexpr (kLdsRng) {
-    __shared__ uint32_t s_rng[(kBlock / 64) * 4 * 64];
-    path.rbw = s_rng + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * 256u;
-  }
-  constexpr bool kPark = Park<F, kMode, kStats>();
-  lds_u32* pk = nullptr;  // this lane's park planes (kPark)
-  if constexpr (kPark) {
-    __shared__ uint32_t s_park[(kBlock / 64) * kParkWords * 64];
-    pk = (lds_u32*)(s_park) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * (kParkWords * 64u) +
-         __lane_id();
-  }
-  path.xy = 0;
+  path.rb = lp + 64u * kRngP;
+  lds_u32* pk = lp + 64u * kParkP;  // this lane's park planes (kPark)
+  path.pix = 0;
   path.start(0);
   path.r0 = path.r1 = path.r2 = path.r3 = 0;
   f3 ro = mk(0, 0, 0), rd = mk(0, 0, 1), thr = mk(1, 1, 1);
@@ -1900,7 +1926,9 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
         bnext = old + count;
       }
       if (need && !idle) {
-        const uint32_t k = (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+        // lanes of `mask` below this one (v_mbcnt: no lane mask held in registers)
+        const uint32_t k = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
         const uint32_t item = k < avail ? old + k : fresh + (k - avail);
         // (no `continue` here: every lane reaches the loop-head ballots below)
         if (item >= A.n_items()) {
@@ -1945,12 +1973,12 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
               const uint32_t phase = rank >= pm ? rank - pm : rank + world - pm;
               y = (per * world + phase) * bh + ((uint32_t)r - per * bh);
             }
-            path.xy = (uint32_t)x | (y << 16);
+            path.pix = y * (uint32_t)A.width() + (uint32_t)x;
             item_rays = 0;
             need = false;
             path.start((uint32_t)f);
             path.sij = ce[1];  // then advanced per frame below
-            camera_ray<F>(P, path, ro, rd, rtime);
+            camera_ray<F>(P, path, (uint32_t)x, y, ro, rd, rtime);
             thr = mk(1, 1, 1);
             const uint32_t s0 = (uint32_t)(f - A.frame_begin()) & (kOctet - 1u);
             dl = max_depth | ((uint32_t)(fstop - f - 1) << 16) | (s0 << 27);
@@ -1980,29 +2008,29 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
         pk_st(pk, kPkDl, dl);
         pk_st(pk, kPkSij, path.sij);
         pk_st(pk, kPkFrame, path.frame);
-        pk_st(pk, kPkXy, path.xy);
+        pk_st(pk, kPkPix, path.pix);
         pk_st(pk, kPkN, path.n);
         pk_st3(pk, kPkO, ro);
         pk_st3(pk, kPkD, rd);
-        ParkedPath pp{path.rbw, pk};
-        hit = trace_linear<F, kStats>(P, ParkRay{pk}, rtime, pp, h, cnt);
+        ParkedPath pp{path.rb, pk};
+        hit = trace_linear<F, kStats>(P, ParkRay{pk}, rtime, pp, h, lp + 64u * kCandP, cnt);
         thr = pk_ld3(pk, kPkThr);
         dl = pk_ld(pk, kPkDl);
         path.sij = pk_ld(pk, kPkSij);
         path.frame = pk_ld(pk, kPkFrame);
-        path.xy = pk_ld(pk, kPkXy);
+        path.pix = pk_ld(pk, kPkPix);
         path.n = pk_ld(pk, kPkN);
         ro = pk_ld3(pk, kPkO);
         rd = pk_ld3(pk, kPkD);
       } else if constexpr (kMode == kModeLinear) {
-        hit = trace_linear<F, kStats>(P, RegRay{ro, rd}, rtime, path, h, cnt);
+        hit = trace_linear<F, kStats>(P, RegRay{ro, rd}, rtime, path, h, lp + 64u * kCandP, cnt);
 #if RT2_EXP_TRACE_TWICE
         {
           f3 ro2 = ro;
           asm volatile("" : "+v"(ro2.x), "+v"(ro2.y), "+v"(ro2.z));
           HitRef h2;
           auto p2 = path;
-          bool hit2 = trace_linear<F, kStats>(P, RegRay{ro2, rd}, rtime, p2, h2, cnt);
+          bool hit2 = trace_linear<F, kStats>(P, RegRay{ro2, rd}, rtime, p2, h2, lp + 64u * kCandP, cnt);
           asm volatile("" ::"v"(h2.t), "v"(h2.prim), "v"(h2.xf), "v"((int)hit2));
         }
 #endif
@@ -2093,13 +2121,15 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
     if (done) {
       // this frame's sample, summed in frame order by accumulate_kernel (RayTracer.cpp:64)
       const LoopArgs A = loop_args();
-      const uint32_t lidx = local_index(A, path.xy);
+      uint32_t px = 0, py = 0;
+      pix_xy(A, path.pix, px, py);
+      const uint32_t lidx = A.world() > 1 ? local_index(A, px, py) : path.pix;
       const uint32_t fr = path.frame - (uint32_t)A.frame_begin();  // launch-relative frame
       const uint32_t slot = fr & (kOctet - 1u);
       float* blk = A.samples() + 3ull * kOctet * ((unsigned long long)(fr / kOctet) * A.local_pixels() + lidx);
       const bool more = ((dl >> 16) & kChunkLeftMask) != 0u;  // frames of the chunk after this one
       if constexpr (kGroup != 0u) {
-        float* oct = oct_wave + __lane_id();
+        lds_f32* oct = (lds_f32*)(lp + 64u * kOctP);
         const uint32_t gs = slot & (kGroup - 1u);  // slot within the group = LDS slot
         if (gs == kGroup - 1u || !more) {
           const uint32_t g0 = slot - gs;  // the group's first octet slot
@@ -2149,11 +2179,11 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
           f3 o2, d2;
           float t2;
           asm volatile("" : "+v"(p2.frame), "+v"(p2.sij));
-          camera_ray<F>(P, p2, o2, d2, t2);
+          camera_ray<F>(P, p2, px, py, o2, d2, t2);
           asm volatile("" ::"v"(o2.x), "v"(d2.x), "v"(d2.y), "v"(d2.z), "v"(t2));
         }
 #endif
-        camera_ray<F>(P, path, ro, rd, rtime);
+        camera_ray<F>(P, path, px, py, ro, rd, rtime);
         thr = mk(1, 1, 1);
         // one frame fewer left; after the octet's last slot the next octet starts at slot 0
         dl = (((dl & 0x07FF0000u) - 0x10000u) | (uint32_t)A.max_depth()) | (slot == kOctet - 1u ? 0u : (dl & 0xF8000000u));
@@ -2279,6 +2309,10 @@ KernelFn PickMode(int mode, bool stats) {
 }
 
 KernelFn Kernel(int v, int mode, bool stats) {
+#ifdef RT2_ONLY_VARIANT  // register-allocation experiments: one threaded product kernel only (not a usable build)
+  (void)v, (void)mode, (void)stats;
+  return reinterpret_cast<KernelFn>(&render_kernel<kVariants[RT2_ONLY_VARIANT], kModeLinear, false>);
+#else
   switch (v) {
     case 0: return PickMode<0>(mode, stats);
     case 1: return PickMode<1>(mode, stats);
@@ -2287,6 +2321,7 @@ KernelFn Kernel(int v, int mode, bool stats) {
     case 4: return PickMode<4>(mode, stats);
   }
   return nullptr;
+#endif
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2295,6 +2330,7 @@ KernelFn Kernel(int v, int mode, bool stats) {
 //   which 3: the same for any quotient with 2^-100 <= |a| < 2^21 (medium box boundaries, any t)
 //   which 1: aabb_hit_fin == aabb_hit for rays with finite inv
 //   which 2: rcp_nr == 1/x and sqrt_nr == sqrt(x) in their ranges
+//   which 4: acc_slab (accelerated-list padded slab) never culls a box the exact padded slab accepts
 __device__ __forceinline__ float rand_float(uint32_t bits, int emin, int emax, uint32_t sel) {
   const int e = emin + (int)(sel % (uint32_t)(emax - emin + 1));
   return __uint_as_float((bits & 0x807FFFFFu) | ((uint32_t)(e + 127) << 23));
@@ -2320,6 +2356,53 @@ __global__ void selftest_kernel(int which, unsigned long long n, uint32_t seed, 
       checked++;
       const float inv = 1.0f / b;
       if (__float_as_uint(div_by_inv(a, b, inv)) != __float_as_uint(q)) bad++;
+    } else if (which == 4) {
+      // acc_slab never culls a box the exact padded slab test accepts; direction components are +-0
+      // with probability 1/4 each (an infinite 1/d), origins often inside the padding band
+      uint32_t s0, s1, s2, s3;
+      philox(seed, 0xACC5u, (uint32_t)idx, (uint32_t)(idx >> 32), 1u, s0, s1, s2, s3);
+      const float lo_x = rand_float(r0, -4, 9, r1), hi_x = lo_x + rand_float(r1, -6, 8, r0 >> 7);
+      const float lo_y = rand_float(r2, -4, 9, r3), hi_y = lo_y + rand_float(r3, -6, 8, r2 >> 7);
+      const float lo_z = rand_float(s0, -4, 9, s1), hi_z = lo_z + rand_float(s1, -6, 8, s0 >> 7);
+      const float pad = fabsf(rand_float(s2, -14, -6, s3));
+      // origin: inside the padding band of a face on about half the axes
+      auto coord = [&](float lo, float hi, uint32_t r) {
+        const uint32_t m = r & 3u;
+        const float u = to_unit(r);
+        if (m == 0u) return hi + pad * u;          // between hi and hi + pad
+        if (m == 1u) return lo - pad * u;          // between lo - pad and lo
+        return lo + (hi - lo) * 3.0f * (u - 0.33f);  // anywhere around the box
+      };
+      const f3 o = mk(coord(lo_x, hi_x, s3), coord(lo_y, hi_y, s2 ^ r3), coord(lo_z, hi_z, s1 ^ r2));
+      f3 d = mk(rand_float(r0 ^ s0, -20, 1, r3), rand_float(r1 ^ s1, -20, 1, s3 >> 3), rand_float(r2 ^ s2, -20, 1, r0));
+      const uint32_t zz = s0 >> 24;
+      if ((zz & 3u) == 0u) d.x = (zz & 64u) ? -0.0f : 0.0f;
+      if (((zz >> 2) & 3u) == 0u) d.y = (zz & 128u) ? -0.0f : 0.0f;
+      if (((zz >> 4) & 3u) == 0u) d.z = (zz & 32u) ? -0.0f : 0.0f;
+      const f3 inv0 = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+      const f3 inv = mk(acc_slab_inv(inv0.x), acc_slab_inv(inv0.y), acc_slab_inv(inv0.z));
+      const f3 pinv = pad * inv;
+      const float tmax = (s3 & 1u) ? FLT_MAX : rand_float(s0 ^ r3, -3, 12, s2);
+      const bool got = acc_slab(mk(lo_x, lo_y, lo_z), mk(hi_x, hi_y, hi_z), o, inv, pinv, 0.001f, tmax);
+      // exact padded slab in double, shrunk by a relative 1e-6 so that rounding at a face is not a miss
+      double t0 = 0.001, t1 = (double)tmax;
+      bool ref = true;
+      const double los[3] = {lo_x, lo_y, lo_z}, his[3] = {hi_x, hi_y, hi_z}, os[3] = {o.x, o.y, o.z},
+                   ds[3] = {d.x, d.y, d.z};
+      for (int k = 0; k < 3; k++) {
+        const double a = los[k] - pad, b = his[k] + pad, w = 1e-6 * (fabs(a) + fabs(b) + 1.0);
+        if (ds[k] == 0.0) {
+          ref = ref && (a + w < os[k] && os[k] < b - w);
+        } else {
+          double u0 = (a + w - os[k]) / ds[k], u1 = (b - w - os[k]) / ds[k];
+          if (u0 > u1) { const double t = u0; u0 = u1; u1 = t; }
+          t0 = t0 > u0 ? t0 : u0;
+          t1 = t1 < u1 ? t1 : u1;
+        }
+      }
+      ref = ref && t0 * (1.0 + 1e-6) < t1 * (1.0 - 1e-6);
+      checked++;
+      if (ref && !got) bad++;
     } else if (which == 2) {
       // rcp_nr / sqrt_nr against IEEE 1/x and sqrt(x) over their whole ranges
       const float x = rand_float(r0, -95, 125, r1);

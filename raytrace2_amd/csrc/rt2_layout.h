@@ -97,6 +97,17 @@ inline constexpr uint32_t make_ref(uint32_t kind, uint32_t off) { return (kind <
 //          centroids along the node's split axis (kind - kAccBvh); children are ACCBVH or
 //          ACCSPHERE refs (an ACCSPHERE ref points at the child's SPHERE record)
 constexpr uint32_t kListLeafOnly = 1u;
+// The reciprocal direction component an accelerated list's padded slab test uses (render.hip lane
+// walk: ax = fma(lo - o, inv, -pad inv), bx = fma(hi - o, inv, pad inv)): inv itself when finite,
+// else +-2^100. With inv = +-inf (d = +-0) the fma form gives NaN or -inf for an origin inside the
+// padding band [lo - pad, hi + pad] and culls the box; with +-2^100 (a power of two: the products are
+// exact) the two bounds get the signs of (lo - pad - o) and (hi + pad - o), so the axis accepts all
+// t >= 0 up to |hi + pad - o| * 2^100 exactly when o lies in the band. That limit only falls below
+// a ray's range when o is within 2^-100 * range of the padded face, a quarter pad or more outside
+// every sphere's reach (the pad carries a 4x margin), so no hit is lost.
+inline constexpr float acc_slab_inv(float inv) {
+  return inv > 0x1p100f ? 0x1p100f : (inv < -0x1p100f ? -0x1p100f : inv);
+}
 constexpr uint32_t kBoundaryAAFlag = 0x80000000u;
 constexpr uint32_t kBoundaryAAMax = 6;
 

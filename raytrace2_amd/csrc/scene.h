@@ -141,6 +141,7 @@ struct CompiledScene {
   std::vector<float> perlin_vec;  // float4 per gradient
   std::vector<int> perlin_perm;
   int max_stack = 0;              // proven traversal-stack bound (entries)
+  bool stack_ok = true;           // max_stack <= kTraversalStack: the stack traversal can run it
   int bvh_nodes = 0, quads = 0, spheres = 0, lists = 0, xforms = 0, media = 0;
   int acc_lists = 0, acc_nodes = 0;  // exact list acceleration trees (rt2_layout.h LISTACC)
   int bvh_depth = 0;
@@ -151,6 +152,11 @@ struct CompiledScene {
 };
 // accelerate_lists = false keeps every list a linear child loop (the reference's own order).
 bool CompileScene(const Scene& s, CompiledScene& out, std::string& err, bool accelerate_lists = true);
+// Accelerated-list trees built by SAH splits are at most this many levels deeper than balanced ones
+// (compile.cpp BuildAcc); CompileSceneWith(..., 0) builds them balanced (depth ceil(log2 n)).
+constexpr int kAccDepthSlack = 2;
+bool CompileSceneWith(const Scene& s, CompiledScene& out, std::string& err, bool accelerate_lists,
+                      int acc_depth_slack);
 
 // Philox4x32-10 (shared constants with the kernel; see render.hip)
 void Philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1);

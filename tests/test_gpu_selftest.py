@@ -9,14 +9,17 @@
   the ranges where the kernel uses them (normalize, ray reciprocals).
 * div_by_inv over any quotient with numerators down to 2^-100 (a medium box boundary uses every t;
   the kernel guards smaller numerators back to IEEE division).
+* acc_slab: the accelerated-list tree's padded slab test (one fma per bound, +-2^100 for an infinite
+  1/d) never culls a box that the exact padded slab test accepts, for rays with direction components
+  of +-0 and origins inside the padding band (the fma form with 1/d = inf culled those).
 """
 import pytest
 
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("which,n", [(0, 1 << 28), (1, 1 << 26), (2, 1 << 28), (3, 1 << 28)],
-                         ids=["div_by_inv", "aabb_fin", "rcp_sqrt_nr", "div_by_inv_any_t"])
+@pytest.mark.parametrize("which,n", [(0, 1 << 28), (1, 1 << 26), (2, 1 << 28), (3, 1 << 28), (4, 1 << 26)],
+                         ids=["div_by_inv", "aabb_fin", "rcp_sqrt_nr", "div_by_inv_any_t", "acc_slab_conservative"])
 def test_selftest(have_gpu, which, n):
     from raytrace2_amd._native import selftest
     bad, checked = selftest(which, n, seed=20241015)

@@ -172,3 +172,50 @@ def test_partition_rows_cover_image_once():
         img = R.assemble_bands(parts, h, bh)
         for r, rr in enumerate(rows):
             assert np.array_equal(img[rr], parts[r])
+
+
+def _graded_list(path, n=400, q=1.2, nest=0):
+    """A sphere list whose centres and radii grow geometrically (x_i = q^i, r_i = 0.01 q^i): the
+    surface-area heuristic peels one sphere off at a time on such a list (an n - 1 level tree), under
+    `nest` levels of transforms."""
+    from raytrace2_amd.authoring import SceneDoc, transform
+    doc = SceneDoc(center=[0, 0, 50], look_at=[0, 0, 0])
+    m = doc.lambertian([0.5, 0.5, 0.5])
+    node = {"transform": transform([0, 0, 0]),
+            "children": [{"primitive": doc.sphere([q ** i, 0.0, 0.0], 0.01 * q ** i, m)} for i in range(n)]}
+    for k in range(nest):
+        node = {"transform": transform([0.1 * k, 0, 0]),
+                "children": [node, {"primitive": doc.sphere([0, -5 - k, 0], 1, m)}]}
+    doc.nodes.append(node)
+    doc.dump(path)
+    return path
+
+
+@pytest.mark.parametrize("q", [1.03, 1.07, 1.2])
+def test_sah_list_tree_depth_is_bounded(tmp_path, q, monkeypatch):
+    """SAH splits had no depth bound, so a size-graded sphere list could make a scene fail
+    to load only because of the heuristic. The tree is now at most kAccDepthSlack (2) levels deeper
+    than the balanced ceil(log2 n) = 9, so its stack need stays near the median split's."""
+    path = _graded_list(str(tmp_path / "graded.json"), q=q)
+    sah = R.Scene(path).info()
+    monkeypatch.setenv("RT2_ACC_SAH", "0")
+    med = R.Scene(path).info()
+    assert sah.acc_lists == med.acc_lists == 1 and sah.acc_nodes == med.acc_nodes == 399
+    assert med.max_stack <= sah.max_stack <= med.max_stack + 2 <= 24
+
+
+@pytest.mark.parametrize("nest", [5, 6, 7])
+def test_scene_loads_whenever_the_balanced_tree_fits(tmp_path, nest, monkeypatch):
+    """With SAH trees the scene loads whenever it loads with balanced (median-split) trees: a stack
+    overflow caused by the SAH's extra depth retries with balanced trees, and a scene whose stack
+    bound exceeds the kernel's 24 entries still loads when it has a threaded program (which needs no
+    stack)."""
+    path = _graded_list(str(tmp_path / "nest.json"), nest=nest)
+    monkeypatch.setenv("RT2_ACC_SAH", "0")
+    med = R.Scene(path).info()
+    monkeypatch.delenv("RT2_ACC_SAH")
+    sah = R.Scene(path).info()
+    assert med.max_stack <= sah.max_stack and (sah.max_stack <= 24 or sah.max_stack == med.max_stack)
+    assert sah.linear_steps == med.linear_steps > 0
+    if nest == 7:
+        assert sah.max_stack > 24  # threaded only (the tracer refuses the stack modes for it)
