@@ -2,7 +2,9 @@
 """Benchmark: Mray/s (samples x bounces) on the Cornell box at 1024^2 @ 1000 spp (BASELINE.json configs[1]).
 
 One step = one full progressive render of the workload: Reset() + spp x Update() (launched as one
-render, rt2.h lazy queue) + the gather of every GPU's row bands into the full image on the root GPU.
+render, rt2.h lazy queue) + the gather of every GPU's row bands into the full image on the root GPU
++ the readback of that image's NonConvertedPixels() into host memory (App.cpp:163-174's headless
+output; pinned, enqueued on the root's stream, complete at the step's closing synchronize).
 Rays = closest-hit queries issued by RayColor (one per bounce level with depth > 0),
 counted by the kernel. The scene program is resident in HBM before timing starts.
 
@@ -232,6 +234,12 @@ def main():
     torch.cuda.set_device(dev)
 
     import raytrace2_amd as R
+    from raytrace2_amd._native import Rt2Error
+
+    def fail(what, e):
+        """A clear non-zero exit naming the C ABI's error text (rt2_last_error), e.g. an RCCL failure."""
+        print(f"bench.py: {what} failed: {e}", file=sys.stderr, flush=True)
+        sys.exit(3)
 
     scene_file = os.path.join(ROOT, "scenes", a.scene)
     if a.scene.startswith("gen:"):  # gen:<generator>:<n>:<seed> -> raytrace2_amd.authoring scene
@@ -242,10 +250,13 @@ def main():
         authoring.GENERATORS[gen](random.Random(int(gseed)), int(n)).dump(scene_file)
     t0 = time.perf_counter()
     sc = R.Scene(scene_file, a.seed)
-    if mode == "multi":
-        tr = R.RayTracer(sc, devices=list(range(n_gpus)), band_h=a.band_h)
-    else:
-        tr = R.RayTracer(sc, local_rank)
+    try:
+        if mode == "multi":  # ncclCommInitAll for n_gpus > 1
+            tr = R.RayTracer(sc, devices=list(range(n_gpus)), band_h=a.band_h)
+        else:
+            tr = R.RayTracer(sc, local_rank)
+    except Rt2Error as e:
+        fail("rt2_tracer_create" + ("_multi" if mode == "multi" else ""), e)
     tr.set_seed(a.seed)
     tr.max_depth = a.max_depth
     tr.SetSamplesPerPixel(a.spp)
@@ -259,7 +270,10 @@ def main():
         else:
             uid = [R.comm_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(uid, src=0)
-            tr.join(uid[0], world, rank, a.band_h)
+            try:
+                tr.join(uid[0], world, rank, a.band_h)  # ncclCommInitRank
+            except Rt2Error as e:
+                fail(f"rt2_tracer_join (rank {rank} of {world})", e)
     if a.launch_frames:
         tr.set_launch_frames(a.launch_frames)
     if a.work_split >= 0:
@@ -269,6 +283,13 @@ def main():
     if a.sample_budget_gb > 0:
         tr.set_sample_budget(int(a.sample_budget_gb * (1 << 30)))
     tr.synchronize()
+    # the root's host copy of the image (NonConvertedPixels, float3): pinned, read back every step
+    readback = None
+    # (an older library in a tools/ A/B run may lack the entry points used below)
+    new_abi = hasattr(R._native.lib, "rt2_tracer_part_stats")
+    if rank == 0 and mode in ("ranks", "multi") and host_gather is None and new_abi:
+        from raytrace2_amd.progressive import PinnedBuffer
+        readback = PinnedBuffer((a.height, a.width, 3), np.float32)
     setup_s = time.perf_counter() - t0
 
     def step():
@@ -279,7 +300,12 @@ def main():
             host_gather.local_view().copy_(torch.from_numpy(tr.Accumulation()))
             host_gather.gather()
         elif mode in ("ranks", "multi"):
-            tr.gather()  # ncclGather of the row bands to rank 0 + de-interleave (rt2_tracer_gather)
+            try:
+                tr.gather()  # ncclGather of the row bands to rank 0 + de-interleave (rt2_tracer_gather)
+            except Rt2Error as e:
+                fail("rt2_tracer_gather (ncclGather)", e)
+            if readback is not None:  # NonConvertedPixels() to the host (App.cpp:163-174)
+                tr.image_non_converted_pixels_async(readback.array.ctypes.data)
 
     def sync_all():
         if mode == "multi":
@@ -314,7 +340,15 @@ def main():
         el, st = timed(a.steps, a.warmup)
         per_rank.append({"rank": er, "rows": tr.local_rows(), "elapsed_s": el, "rays": st["rays"],
                          "kernel_ms": st["kernel_ms"], "launches": st["launches"], "gather_ms": st["gather_ms"],
-                         "gathers": st["gathers"], "mray_s": st["rays"] / el / 1e6})
+                         "gathers": st["gathers"], "enqueue_ms": st.get("enqueue_ms", 0.0),
+                         "readbacks": st.get("readbacks", 0), "readback_ms": st.get("readback_ms", 0.0),
+                         "mray_s": st["rays"] / el / 1e6})
+        if mode == "multi" and new_abi:  # each GPU of the one-process tracer
+            per_rank[-1]["gpus"] = []
+            for g in range(n_gpus):
+                ps = tr.part_stats(g)
+                per_rank[-1]["gpus"].append({"gpu": g, "rays": ps["rays"], "kernel_ms": ps["kernel_ms"],
+                                             "enqueue_ms": ps["enqueue_ms"], "launches": ps["launches"]})
     launch_shape = tr.last_launch()  # the timed launches' shape (before the stats pass below)
     me = per_rank[-1] if mode != "emulate" else max(per_rank, key=lambda r: r["elapsed_s"])
     if mode == "ranks":
@@ -399,6 +433,9 @@ def main():
                        "kernel_sha": key["kernel_sha"], "source_kernel_sha": src_sha,
                        "kernel_ms_per_step_max": round(max(r["kernel_ms"] for r in per_rank) / a.steps, 2),
                        "gather_ms_per_step": round(per_rank[0]["gather_ms"] / a.steps, 3),
+                       "readback_ms_per_step": round(per_rank[0]["readback_ms"] / a.steps, 3),
+                       "readback_bytes_per_step": (a.width * a.height * 12 if per_rank[0]["readbacks"] else 0),
+                       "enqueue_ms_per_step": round(per_rank[0]["enqueue_ms"] / a.steps, 3),
                        "per_rank": [{"rank": r["rank"], "rows": r["rows"], "mray_s": round(r["mray_s"], 1),
                                      "ms_per_step": round(r["elapsed_s"] * 1e3 / a.steps, 2),
                                      "kernel_ms_per_step": round(r["kernel_ms"] / a.steps, 2)} for r in per_rank],
@@ -408,6 +445,18 @@ def main():
         }
         if cpu:
             out["detail"]["gpu_over_cpu"] = round(value / cpu["value"], 1)
+        # per GPU (N > 1): kernel time and rays of each GPU, the host time of its launches' enqueue,
+        # and the slowest / fastest GPU kernel-time ratio (the load balance of the row-band split)
+        gpus = per_rank[0].get("gpus") if mode == "multi" else (
+            [{"gpu": r["rank"], "rays": r["rays"], "kernel_ms": r["kernel_ms"], "enqueue_ms": r["enqueue_ms"],
+              "launches": r["launches"]} for r in per_rank] if mode == "ranks" else None)
+        if gpus:
+            out["detail"]["per_gpu"] = [{"gpu": g["gpu"], "rays": int(g["rays"]),
+                                         "kernel_ms_per_step": round(g["kernel_ms"] / a.steps, 3),
+                                         "enqueue_ms_per_step": round(g["enqueue_ms"] / a.steps, 3),
+                                         "launches": g["launches"]} for g in gpus]
+            ks = [g["kernel_ms"] for g in gpus]
+            out["detail"]["slowest_over_fastest_gpu"] = round(max(ks) / max(1e-9, min(ks)), 4)
         if mode == "emulate":
             out["config"]["emulated"] = (f"{len(per_rank)} rank(s) of {a.emulate_world} timed one after another on "
                                          "this GPU; value = their rays / the slowest rank's time (no gather)")

@@ -183,12 +183,26 @@ RT2_API int rt2_tracer_get_camera(const rt2_tracer* tr, rt2_camera_desc* out);
 RT2_API int rt2_tracer_create_multi(const rt2_scene* scene, int n_gpus, const int* devices, int band_h,
                                     rt2_tracer** out);
 RT2_API int rt2_tracer_n_gpus(const rt2_tracer* tr); /* devices of a multi tracer, else 1 */
+/* rt2_tracer_create_multi's argument checks and partition, on the host only (no GPU, no RCCL): part
+ * i = rank i on devices[i] renders local_rows rows of the image in bands of band_h rows (0 = 2), and
+ * every part sends rows_max rows in the gather. loopback = 1 when every device is one GPU (the tests'
+ * configuration: device-local copies instead of RCCL). out may be NULL (checks only). */
+typedef struct {
+  int device, rank, world, band_h;
+  int local_rows; /* image rows this part renders */
+  int rows_max;   /* rows of the largest part's band stack: what every part sends */
+} rt2_part_plan;
+RT2_API int rt2_multi_plan(int n_gpus, const int* devices, int band_h, int width, int height, rt2_part_plan* out,
+                           int* loopback);
 RT2_API int rt2_comm_unique_id(uint8_t* out, size_t cap); /* cap >= RT2_UNIQUE_ID_BYTES */
 RT2_API int rt2_tracer_join(rt2_tracer* tr, const uint8_t* unique_id, int world, int rank, int band_h);
 RT2_API int rt2_tracer_gather(rt2_tracer* tr);
 /* Root (rank 0 / a multi tracer) after a gather: the full image, rows bottom-up, H x W. */
 RT2_API int rt2_tracer_image_accumulation(rt2_tracer* tr, float* out);        /* raw float3 sums */
 RT2_API int rt2_tracer_image_non_converted_pixels(rt2_tracer* tr, float* out); /* accum / frame_idx */
+/* NonConvertedPixels of the gathered image enqueued on the root's stream into pinned host memory
+ * (rt2_host_alloc); complete when rt2_tracer_query returns 1 or after rt2_tracer_synchronize. */
+RT2_API int rt2_tracer_image_non_converted_pixels_async(rt2_tracer* tr, float* out);
 RT2_API int rt2_tracer_image_pixels(rt2_tracer* tr, uint8_t* out_rgba);       /* Pixels(): RGBA8 */
 /* The gather's layout, for callers that move the band stacks themselves (e.g. over another
  * collective library): every rank sends rt2_band_rows_max(height, band_h, world) rows of its band
@@ -223,8 +237,15 @@ typedef struct {
    * and kernel_ms (the largest per-GPU sum). */
   uint64_t gathers;
   double gather_ms;
+  /* host time spent enqueueing renders (a multi-GPU tracer: sum over its GPUs); image readbacks to
+   * the host (rt2_tracer_image_*) on the root and their device-to-host copy time */
+  double enqueue_ms;
+  uint64_t readbacks;
+  double readback_ms;
 } rt2_stats;
 RT2_API int rt2_tracer_get_stats(rt2_tracer* tr, rt2_stats* out);
+/* The stats of GPU `part` of a multi-GPU tracer (part 0 of a one-GPU tracer is itself). */
+RT2_API int rt2_tracer_part_stats(rt2_tracer* tr, int part, rt2_stats* out);
 RT2_API int rt2_tracer_reset_stats(rt2_tracer* tr);
 
 /* Diagnostic: checks the kernel's exact arithmetic shortcuts against their reference form on n

@@ -160,6 +160,8 @@ class OracleScene:
 CTL_WORLD_T = 1      # transformed children report world-space t (Transform.cpp:13-20,75-88 quirk removed)
 CTL_SINGLE_LEAF = 2  # span-1 BVH leaves tested once (BVH.cpp:18-20,50-55 quirk removed)
 CTL_INF = 4          # kInfinity = +inf instead of FLT_MAX (Defs.hpp:17)
+# ... and one that RESTORES the reference's sampling and libm calls where the restatement deviates
+CTL_REF_MATH = 8     # rejection RandInUnitSphere/Disk, std::log, std::sin(float), std::pow(double, 5)
 
 
 class controls:

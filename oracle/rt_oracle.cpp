@@ -53,7 +53,13 @@ using real = float;
 //      of the model-space t of Transform.cpp:13-20,75-88
 //   2: a span-1 BVH leaf is tested once, not twice (BVH.cpp:18-20, 50-55)
 //   4: kInfinity = +inf instead of FLT_MAX (Defs.hpp:17)
-enum : int { kCtlWorldT = 1, kCtlSingleLeaf = 2, kCtlInf = 4 };
+// and one bit that RESTORES the reference's own sampling and libm calls where the restatement
+// deviates on purpose (DESIGN.md §2 "Deliberate deviations"), to measure those deviations:
+//   8: RandInUnitSphere / RandInUnitDisk by rejection on the same Philox stream (Math.hpp:26-43),
+//      std::log(float) in ConstantMedium (ConstantMedium.cpp:42), std::sin(float) in the marble
+//      texture (Texture.cpp:16), glm::pow(1 - cos, 5) = std::pow(double, int) in Schlick
+//      (Material.cpp:24; glm's scalar pow is std::pow, and (float, int) promotes to double)
+enum : int { kCtlWorldT = 1, kCtlSingleLeaf = 2, kCtlInf = 4, kCtlRefMath = 8 };
 static int g_controls = 0;
 #define kInfinity ((g_controls & kCtlInf) ? (real)INFINITY : (real)FLT_MAX)  // Defs.hpp:17
 
@@ -303,6 +309,14 @@ inline float LogU(float u) {
 // (a rejection loop costs a GPU wave its unluckiest lane's retries): z = 1 - 2u, phi = 2 pi v;
 // r = sqrt(u), phi = 2 pi v.
 inline vec3 RandUnitVec3(Rng& g) {
+  if (g_controls & kCtlRefMath) {  // Math.hpp:26-32, 45: normalize(RandInUnitSphere())
+    while (true) {
+      const float x = g.RandReal(-1, 1), y = g.RandReal(-1, 1), z = g.RandReal(-1, 1);
+      const vec3 p{x, y, z};
+      const float length_sq = dot(p, p);
+      if (1e-160 < (double)length_sq && (double)length_sq <= 1.0) return normalize(p);
+    }
+  }
   const float u = g.RandReal();
   const float v = g.RandReal();
   const float z = 1.0f - 2.0f * u;
@@ -312,6 +326,13 @@ inline vec3 RandUnitVec3(Rng& g) {
   return {r * c, r * s, z};
 }
 inline vec3 RandInUnitDisk(Rng& g) {
+  if (g_controls & kCtlRefMath) {  // Math.hpp:34-41 (arguments drawn left to right)
+    while (true) {
+      const float x = g.RandReal(-1, 1), y = g.RandReal(-1, 1);
+      const vec3 p{x, y, 0.0f};
+      if ((double)dot(p, p) < 1.0) return p;
+    }
+  }
   const float u = g.RandReal();
   const float v = g.RandReal();
   const float r = std::sqrt(u);
@@ -612,7 +633,8 @@ struct ConstantMedium : Hittable {
     rec1.t = (float)std::fmax((double)rec1.t, 0.0);
     float ray_len = length(r.direction);
     float dist_inside = (rec2.t - rec1.t) * ray_len;
-    float hit_dist = neg_inv_density * LogU(c.rng->RandReal());
+    const float u = c.rng->RandReal();
+    float hit_dist = neg_inv_density * ((g_controls & kCtlRefMath) ? std::log(u) : LogU(u));
     if (hit_dist > dist_inside) return false;
     rec.t = rec1.t + hit_dist / ray_len;
     rec.point = r.At(rec.t);
@@ -809,6 +831,7 @@ vec3 TexValue(const Scene& s, uint32_t idx, vec3 p) {
     case kNoise:
       if (t.noise_type == 1) {
         float arg = t.scale * p.z + 10 * t.perlin->Turb(p);
+        if (g_controls & kCtlRefMath) return (t.albedo * 0.5f) * (1 + std::sin(arg));  // sinf (Texture.cpp:16)
         return (t.albedo * 0.5f) * (1 + (float)std::sin((double)arg));
       }
       return (t.albedo * 0.5f) * (1.0f + t.perlin->Noise(t.scale * p));
@@ -840,6 +863,7 @@ bool Scatter(const Scene& s, Rng& g, const Ray& r_in, const HitRecord& rec, vec3
         double x = (double)(1 - cos_theta);
         double x2 = x * x;
         double x5 = (x2 * x2) * x;
+        if (g_controls & kCtlRefMath) x5 = std::pow((double)(1 - cos_theta), 5);  // Material.cpp:24
         double schlick = (double)r0 + (double)(1 - r0) * x5;
         reflect = schlick > (double)g.RandReal();
       }

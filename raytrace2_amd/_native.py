@@ -47,6 +47,10 @@ class AppSettings(ctypes.Structure):
                 ("render_window", ctypes.c_int)]
 
 
+class PartPlan(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in ("device", "rank", "world", "band_h", "local_rows", "rows_max")]
+
+
 class Stats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in
                 ("rays", "paths", "bvh_tests", "quad_tests", "sphere_tests", "xform_visits",
@@ -54,10 +58,13 @@ class Stats(ctypes.Structure):
                                                                            ("stamps", ctypes.c_uint64 * 4),
                                                                            ("diag", ctypes.c_uint64 * 8),
                                                                            ("gathers", ctypes.c_uint64),
-                                                                           ("gather_ms", ctypes.c_double)]
+                                                                           ("gather_ms", ctypes.c_double),
+                                                                           ("enqueue_ms", ctypes.c_double),
+                                                                           ("readbacks", ctypes.c_uint64),
+                                                                           ("readback_ms", ctypes.c_double)]
 
     def as_dict(self):
-        d = {n: (getattr(self, n) if n in ("kernel_ms", "gather_ms") else int(getattr(self, n))) for n, _ in self._fields_
+        d = {n: (getattr(self, n) if n.endswith("_ms") else int(getattr(self, n))) for n, _ in self._fields_
              if n not in ("stamps", "diag")}
         d["stamps"] = [int(x) for x in self.stamps]
         d["diag"] = [int(x) for x in self.diag]
@@ -135,6 +142,10 @@ def _load():
         "rt2_tracer_ray_counts": (i32, [vp, ctypes.POINTER(ctypes.c_uint32)]),
         "rt2_tracer_enable_stats": (i32, [vp, i32]),
         "rt2_tracer_get_stats": (i32, [vp, ctypes.POINTER(Stats)]),
+        "rt2_tracer_part_stats": (i32, [vp, i32, ctypes.POINTER(Stats)]),
+        "rt2_multi_plan": (i32, [i32, ctypes.POINTER(ctypes.c_int), i32, i32, i32, ctypes.POINTER(PartPlan),
+                                 ctypes.POINTER(ctypes.c_int)]),
+        "rt2_tracer_image_non_converted_pixels_async": (i32, [vp, vp]),
         "rt2_tracer_reset_stats": (i32, [vp]),
         "rt2_write_image": (i32, [fp, i32, i32, ctypes.c_char_p, i32]),
         "rt2_tracer_set_camera": (i32, [vp, ctypes.POINTER(CameraDesc)]),
@@ -153,6 +164,8 @@ def _load():
         "rt2_runtime_info": (i32, [ctypes.c_char_p, ctypes.c_size_t]),
     }
     for name, (res, args) in sig.items():
+        if not hasattr(L, name):  # an older library (tools/ A/B runs of earlier builds): absent entry points
+            continue
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
@@ -174,6 +187,16 @@ def selftest(which: int, n: int, seed: int = 1, device: int = 0):
     bad, checked = ctypes.c_uint64(0), ctypes.c_uint64(0)
     check(lib.rt2_selftest(device, which, n, seed, ctypes.byref(bad), ctypes.byref(checked)))
     return bad.value, checked.value
+
+
+def multi_plan(n_gpus: int, devices=None, band_h: int = 0, width: int = 0, height: int = 0):
+    """rt2_multi_plan: rt2_tracer_create_multi's argument checks and per-GPU partition, on the host
+    (no GPU, no RCCL). Returns (list of part dicts, loopback)."""
+    plans = (PartPlan * max(1, n_gpus))()
+    devs = (ctypes.c_int * len(devices))(*devices) if devices is not None else None
+    lb = ctypes.c_int(0)
+    check(lib.rt2_multi_plan(n_gpus, devs, band_h, width, height, plans, ctypes.byref(lb)))
+    return [{f: getattr(plans[i], f) for f, _ in PartPlan._fields_} for i in range(n_gpus)], bool(lb.value)
 
 
 def runtime_info() -> str:

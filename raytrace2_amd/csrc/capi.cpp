@@ -8,6 +8,7 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -30,7 +31,7 @@ int RenderVariant(uint32_t features);
 uint32_t RenderVariantFeatures(int v);
 size_t RenderLdsBytes(const RenderParams& p);
 bool WriteImage(const float* pixels, int w, int h, const std::string& path, bool png, std::string& err);
-hipError_t LaunchDeinterleave(const float* stacks, float* image, uint8_t* pixels, int width, int height, int band_h,
+hipError_t LaunchDeinterleave(const float* stacks, float* image, float* image_nc, uint8_t* pixels, int width, int height, int band_h,
                               int world, int max_rows, int frame_idx, hipStream_t stream);
 }  // namespace rt2
 
@@ -126,12 +127,18 @@ struct rt2_tracer {
   // root (rank 0) image: the gathered band stacks and the de-interleaved full image
   float* d_stacks = nullptr;      // [world][max_rows][W] float3
   float* d_image = nullptr;       // [H][W] float3
+  float* d_image_nc = nullptr;    // [H][W] float3 NonConvertedPixels() = image / frame_idx
   uint8_t* d_image_px = nullptr;  // [H][W] RGBA8
   size_t stacks_bytes = 0, image_pixels = 0;
   int64_t image_frame = -1;  // frame index of the last gather (-1: none since the last resize/reset)
   uint64_t gathers = 0;
   double gather_ms = 0;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> gpending;  // per-gather timing events
+  // image readbacks to the host (rt2_tracer_image_*): count and device-to-host copy time
+  uint64_t readbacks = 0;
+  double readback_ms = 0;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> rpending;  // async readbacks' timing events
+  double enqueue_ms = 0;  // host time spent enqueueing this tracer's renders (LaunchFrames)
 };
 
 namespace {
@@ -185,9 +192,11 @@ int AllocRows(const rt2_tracer* t) { return BandRowsMax(t); }
 void FreeImage(rt2_tracer* t) {
   (void)hipFree(t->d_stacks);
   (void)hipFree(t->d_image);
+  (void)hipFree(t->d_image_nc);
   (void)hipFree(t->d_image_px);
   t->d_stacks = nullptr;
   t->d_image = nullptr;
+  t->d_image_nc = nullptr;
   t->d_image_px = nullptr;
   t->stacks_bytes = 0;
   t->image_pixels = 0;
@@ -261,6 +270,15 @@ int DrainEvents(rt2_tracer* t) {
     t->event_pool.push_back(pr.second);
   }
   t->gpending.clear();
+  for (auto& pr : t->rpending) {
+    HIP_TRY(hipEventSynchronize(pr.second));
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, pr.first, pr.second));
+    t->readback_ms += ms;
+    t->event_pool.push_back(pr.first);
+    t->event_pool.push_back(pr.second);
+  }
+  t->rpending.clear();
   return RT2_OK;
 }
 
@@ -557,6 +575,10 @@ void rt2_tracer_destroy(rt2_tracer* t) {
   if (t->stream) (void)hipStreamSynchronize(t->stream);
   if (t->comm) (void)ncclCommDestroy(t->comm);
   for (auto& pr : t->gpending) {
+    (void)hipEventDestroy(pr.first);
+    (void)hipEventDestroy(pr.second);
+  }
+  for (auto& pr : t->rpending) {
     (void)hipEventDestroy(pr.first);
     (void)hipEventDestroy(pr.second);
   }
@@ -1069,7 +1091,10 @@ int Flush(rt2_tracer* t) {
   if (t->queued == 0) return RT2_OK;
   const int n = t->queued;
   t->queued = 0;
-  return LaunchFrames(t, n);
+  const auto t0 = std::chrono::steady_clock::now();
+  const int rc = LaunchFrames(t, n);
+  t->enqueue_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return rc;
 }
 
 // ---- multi-GPU gather ----
@@ -1082,6 +1107,7 @@ int EnsureImage(rt2_tracer* root) {
   HIP_TRY(hipSetDevice(root->device));
   HIP_TRY(hipMalloc(&root->d_stacks, std::max<size_t>(stacks, 4)));
   HIP_TRY(hipMalloc(&root->d_image, std::max<size_t>(npix * 3 * sizeof(float), 4)));
+  HIP_TRY(hipMalloc(&root->d_image_nc, std::max<size_t>(npix * 3 * sizeof(float), 4)));
   HIP_TRY(hipMalloc(&root->d_image_px, std::max<size_t>(npix * 4, 4)));
   root->stacks_bytes = stacks;
   root->image_pixels = npix;
@@ -1154,7 +1180,8 @@ int GatherRanks(const std::vector<rt2_tracer*>& ranks, bool loopback) {
   }
   if (root) {
     HIP_TRY(hipSetDevice(root->device));
-    HIP_TRY(LaunchDeinterleave(root->d_stacks, root->d_image, root->d_image_px, root->width, root->height,
+    HIP_TRY(LaunchDeinterleave(root->d_stacks, root->d_image, root->d_image_nc, root->d_image_px, root->width,
+                               root->height,
                                BandH(root), root->world, BandRowsMax(root), (int)root->frame_idx, root->stream));
     if (e1) HIP_TRY(hipEventRecord(e1, root->stream));
     if (e0 && e1) root->gpending.emplace_back(e0, e1);
@@ -1431,6 +1458,9 @@ int rt2_tracer_get_stats(rt2_tracer* t, rt2_stats* o) {
       for (int k = 0; k < 8; k++) sum.diag[k] += s.diag[k];
       sum.gathers += s.gathers;
       sum.gather_ms += s.gather_ms;
+      sum.enqueue_ms += s.enqueue_ms;
+      sum.readbacks += s.readbacks;
+      sum.readback_ms += s.readback_ms;
     }
     *o = sum;
     return RT2_OK;
@@ -1455,24 +1485,59 @@ int rt2_tracer_get_stats(rt2_tracer* t, rt2_stats* o) {
   o->kernel_ms = t->kernel_ms;
   o->gathers = t->gathers;
   o->gather_ms = t->gather_ms;
+  o->enqueue_ms = t->enqueue_ms;
+  o->readbacks = t->readbacks;
+  o->readback_ms = t->readback_ms;
   return RT2_OK;
 }
 
+int rt2_tracer_part_stats(rt2_tracer* t, int part, rt2_stats* o) {
+  if (!t || !o) return Fail(RT2_ERR_INVALID, "null argument");
+  const int n = IsMulti(t) ? (int)t->parts.size() : 1;
+  if (part < 0 || part >= n) return Fail(RT2_ERR_INVALID, "rt2_tracer_part_stats: part out of range");
+  return rt2_tracer_get_stats(IsMulti(t) ? t->parts[(size_t)part] : t, o);
+}
+
 // ---- multi-GPU entry points ----
-int rt2_tracer_create_multi(const rt2_scene* s, int n, const int* devices, int band_h, rt2_tracer** out) {
-  if (!s || !out) return Fail(RT2_ERR_INVALID, "rt2_tracer_create_multi: null argument");
-  *out = nullptr;
+int rt2_multi_plan(int n, const int* devices, int band_h, int width, int height, rt2_part_plan* out, int* loopback) {
   if (n < 1 || band_h < 0) return Fail(RT2_ERR_INVALID, "rt2_tracer_create_multi: need n_gpus >= 1, band_h >= 0");
+  if (width < 0 || height < 0) return Fail(RT2_ERR_INVALID, "rt2_multi_plan: negative dims");
   std::vector<int> devs((size_t)n);
   for (int i = 0; i < n; i++) devs[(size_t)i] = devices ? devices[i] : i;
+  for (int d : devs)
+    if (d < 0) return Fail(RT2_ERR_INVALID, "rt2_tracer_create_multi: negative device id");
   const bool all_same = std::all_of(devs.begin(), devs.end(), [&](int d) { return d == devs[0]; });
   std::vector<int> sorted = devs;
   std::sort(sorted.begin(), sorted.end());
   const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
   if (!distinct && !all_same)
     return Fail(RT2_ERR_INVALID, "rt2_tracer_create_multi: devices must be distinct (or all one GPU, for tests)");
+  const int bh = band_h > 0 ? band_h : kDefaultBandH;
+  if (loopback) *loopback = n > 1 && all_same ? 1 : 0;
+  if (out) {
+    for (int i = 0; i < n; i++) {
+      rt2_part_plan& q = out[i];
+      q.device = devs[(size_t)i];
+      q.rank = i;
+      q.world = n;
+      q.band_h = bh;
+      q.local_rows = height > 0 ? LocalRows(height, bh, i, n) : 0;
+      q.rows_max = rt2::BandRowsMax(height, bh, n);
+    }
+  }
+  return RT2_OK;
+}
+
+int rt2_tracer_create_multi(const rt2_scene* s, int n, const int* devices, int band_h, rt2_tracer** out) {
+  if (!s || !out) return Fail(RT2_ERR_INVALID, "rt2_tracer_create_multi: null argument");
+  *out = nullptr;
+  int lb = 0;
+  int prc = rt2_multi_plan(n, devices, band_h, 0, 0, nullptr, &lb);
+  if (prc != RT2_OK) return prc;
+  std::vector<int> devs((size_t)n);
+  for (int i = 0; i < n; i++) devs[(size_t)i] = devices ? devices[i] : i;
   auto m = std::make_unique<rt2_tracer>();
-  m->loopback = n > 1 && all_same;
+  m->loopback = lb != 0;
   const int bh = band_h > 0 ? band_h : kDefaultBandH;
   auto cleanup = [&](int rc) {
     for (rt2_tracer* p : m->parts) rt2_tracer_destroy(p);
@@ -1537,13 +1602,36 @@ int rt2_tracer_image_accumulation(rt2_tracer* t, float* out) {
   return RT2_OK;
 }
 
+// NonConvertedPixels() of the gathered image: accumulation / frame_idx_ (RayTracer.cpp:108-109),
+// divided on the GPU by the de-interleave kernel (the same IEEE quotient as the host's)
 int rt2_tracer_image_non_converted_pixels(rt2_tracer* t, float* out) {
-  int rc = rt2_tracer_image_accumulation(t, out);
+  if (!t || !out) return Fail(RT2_ERR_INVALID, "null argument");
+  rt2_tracer* r = nullptr;
+  int rc = ImageRoot(t, &r);
   if (rc != RT2_OK) return rc;
+  const size_t n = (size_t)r->width * (size_t)r->height;
+  const auto t0 = std::chrono::steady_clock::now();
+  if (n) HIP_TRY(hipMemcpy(out, r->d_image_nc, n * 3 * sizeof(float), hipMemcpyDeviceToHost));
+  r->readback_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  r->readbacks++;
+  return RT2_OK;
+}
+
+// The same, enqueued on the root's stream (out: pinned host memory, rt2_host_alloc); complete once
+// rt2_tracer_query returns 1 or after rt2_tracer_synchronize. Needs a gather enqueued before it.
+int rt2_tracer_image_non_converted_pixels_async(rt2_tracer* t, float* out) {
+  if (!t || !out) return Fail(RT2_ERR_INVALID, "null argument");
   rt2_tracer* r = IsMulti(t) ? t->parts[0] : t;
-  size_t n = (size_t)r->width * (size_t)r->height * 3;
-  float f = (float)r->image_frame;  // accumulation / frame_idx_ (RayTracer.cpp:108-109)
-  for (size_t i = 0; i < n; i++) out[i] = out[i] / f;
+  if (r->rank != 0) return Fail(RT2_ERR_INVALID, "the gathered image lives on rank 0");
+  if (r->image_frame < 0) return Fail(RT2_ERR_INVALID, "no gathered image (call rt2_tracer_gather first)");
+  HIP_TRY(hipSetDevice(r->device));
+  const size_t n = (size_t)r->width * (size_t)r->height;
+  hipEvent_t e0 = TakeEvent(r), e1 = TakeEvent(r);
+  if (e0) HIP_TRY(hipEventRecord(e0, r->stream));
+  if (n) HIP_TRY(hipMemcpyAsync(out, r->d_image_nc, n * 3 * sizeof(float), hipMemcpyDeviceToHost, r->stream));
+  if (e1) HIP_TRY(hipEventRecord(e1, r->stream));
+  if (e0 && e1) r->rpending.emplace_back(e0, e1);
+  r->readbacks++;
   return RT2_OK;
 }
 
@@ -1588,6 +1676,9 @@ int rt2_tracer_reset_stats(rt2_tracer* t) {
   t->kernel_ms = 0;
   t->gathers = 0;
   t->gather_ms = 0;
+  t->enqueue_ms = 0;
+  t->readbacks = 0;
+  t->readback_ms = 0;
   return RT2_OK;
 }
 

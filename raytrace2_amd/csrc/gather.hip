@@ -21,6 +21,7 @@ __device__ __forceinline__ float gmin1(float x, float y) { return y < x ? y : x;
 
 // One thread per image pixel: coalesced reads of one band-stack row, coalesced writes of one image row.
 __global__ __launch_bounds__(256) void deinterleave_kernel(const float* __restrict__ stacks, float* __restrict__ image,
+                                                           float* __restrict__ image_nc,
                                                            uint32_t* __restrict__ pixels, uint32_t width,
                                                            uint32_t npix, uint32_t band_h, uint32_t world,
                                                            uint32_t max_rows, int frame_idx) {
@@ -33,10 +34,14 @@ __global__ __launch_bounds__(256) void deinterleave_kernel(const float* __restri
   image[3ull * i] = a0;
   image[3ull * i + 1] = a1;
   image[3ull * i + 2] = a2;
+  // NonConvertedPixels() (RayTracer.cpp:108-109): accumulation / frame_idx_ in float
+  const float fi = (float)frame_idx;
+  const float cc[3] = {a0 / fi, a1 / fi, a2 / fi};
+  image_nc[3ull * i] = cc[0];
+  image_nc[3ull * i + 1] = cc[1];
+  image_nc[3ull * i + 2] = cc[2];
   uint32_t rgba = 0u;  // Reset() state: nothing rendered yet
   if (frame_idx > 0) {
-    const float fi = (float)frame_idx;
-    const float cc[3] = {a0 / fi, a1 / fi, a2 / fi};
     rgba = 0xFF000000u;
 #pragma unroll
     for (int k = 0; k < 3; k++) {
@@ -49,12 +54,12 @@ __global__ __launch_bounds__(256) void deinterleave_kernel(const float* __restri
 
 }  // namespace dev
 
-hipError_t LaunchDeinterleave(const float* stacks, float* image, uint8_t* pixels, int width, int height, int band_h,
-                              int world, int max_rows, int frame_idx, hipStream_t stream) {
+hipError_t LaunchDeinterleave(const float* stacks, float* image, float* image_nc, uint8_t* pixels, int width,
+                              int height, int band_h, int world, int max_rows, int frame_idx, hipStream_t stream) {
   const uint32_t npix = (uint32_t)width * (uint32_t)height;
   if (npix == 0) return hipSuccess;
   hipLaunchKernelGGL(dev::deinterleave_kernel, dim3((npix + 255u) / 256u), dim3(256), 0, stream, stacks, image,
-                     reinterpret_cast<uint32_t*>(pixels), (uint32_t)width, npix, (uint32_t)band_h, (uint32_t)world,
+                     image_nc, reinterpret_cast<uint32_t*>(pixels), (uint32_t)width, npix, (uint32_t)band_h, (uint32_t)world,
                      (uint32_t)max_rows, frame_idx);
   return hipGetLastError();
 }

@@ -2361,10 +2361,11 @@ __global__ void selftest_kernel(int which, unsigned long long n, uint32_t seed, 
       // with probability 1/4 each (an infinite 1/d), origins often inside the padding band
       uint32_t s0, s1, s2, s3;
       philox(seed, 0xACC5u, (uint32_t)idx, (uint32_t)(idx >> 32), 1u, s0, s1, s2, s3);
-      const float lo_x = rand_float(r0, -4, 9, r1), hi_x = lo_x + rand_float(r1, -6, 8, r0 >> 7);
-      const float lo_y = rand_float(r2, -4, 9, r3), hi_y = lo_y + rand_float(r3, -6, 8, r2 >> 7);
-      const float lo_z = rand_float(s0, -4, 9, s1), hi_z = lo_z + rand_float(s1, -6, 8, s0 >> 7);
-      const float pad = fabsf(rand_float(s2, -14, -6, s3));
+      const float lo_x = rand_float(r0, -4, 9, r1), hi_x = lo_x + fabsf(rand_float(r1, -6, 8, r0 >> 7));
+      const float lo_y = rand_float(r2, -4, 9, r3), hi_y = lo_y + fabsf(rand_float(r3, -6, 8, r2 >> 7));
+      const float lo_z = rand_float(s0, -4, 9, s1), hi_z = lo_z + fabsf(rand_float(s1, -6, 8, s0 >> 7));
+      const float pad = fabsf(rand_float(s2, -14, -6, s3));  // (the same test with 1/d = inf unclamped:
+                                                             // 8 % of these inputs wrongly culled)
       // origin: inside the padding band of a face on about half the axes
       auto coord = [&](float lo, float hi, uint32_t r) {
         const uint32_t m = r & 3u;

@@ -400,5 +400,16 @@ class RayTracer:
         check(lib.rt2_tracer_get_stats(self._h, ctypes.byref(s)))
         return s.as_dict()
 
+    def part_stats(self, part: int) -> dict:
+        """Stats of GPU `part` of a multi-GPU tracer (rt2_tracer_part_stats)."""
+        s = Stats()
+        check(lib.rt2_tracer_part_stats(self._h, part, ctypes.byref(s)))
+        return s.as_dict()
+
+    def image_non_converted_pixels_async(self, out_ptr: int) -> None:
+        """NonConvertedPixels of the gathered image into pinned host memory at out_ptr (rt2_host_alloc,
+        height * width * 3 floats), enqueued; complete after synchronize() or query() == 1."""
+        check(lib.rt2_tracer_image_non_converted_pixels_async(self._h, ctypes.c_void_p(out_ptr)))
+
     def reset_stats(self) -> None:
         check(lib.rt2_tracer_reset_stats(self._h))

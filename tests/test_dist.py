@@ -91,3 +91,32 @@ def test_c_abi_deinterleave_inverts_the_partition(h, band_h, world):
         stacks[r, :len(p)] = p
     img = deinterleave(stacks, h, band_h)
     assert np.array_equal(img.view(np.uint32), assemble_bands(parts, h, band_h).view(np.uint32))
+
+
+@pytest.mark.parametrize("n,height,band_h", [(8, 1024, 0), (8, 1080, 2), (4, 45, 8), (2, 7, 3), (3, 1, 0), (1, 1024, 0)])
+def test_multi_plan_partition_for_distinct_devices(n, height, band_h):
+    """rt2_tracer_create_multi's argument checks and per-GPU partition (rt2_multi_plan), on the host:
+    N distinct device ids without initialising RCCL or touching a GPU. Part i is rank i on device i,
+    its rows are the Python statement of the band partition, and every part sends rows_max rows (whole
+    bands for every period) in the gather."""
+    from raytrace2_amd._native import multi_plan
+    from raytrace2_amd.tracer import local_rows
+    devices = list(range(n))[::-1]  # any distinct ids
+    parts, loopback = multi_plan(n, devices, band_h, 1024, height)
+    assert not loopback and len(parts) == n
+    bh = band_h or 2
+    rows = [len(local_rows(height, bh, r, n)) for r in range(n)]
+    assert [p["device"] for p in parts] == devices and [p["rank"] for p in parts] == list(range(n))
+    assert all(p["world"] == n and p["band_h"] == bh for p in parts)
+    assert [p["local_rows"] for p in parts] == rows and sum(rows) == height
+    bands = -(-height // bh)
+    assert all(p["rows_max"] == -(-bands // n) * bh >= max(rows) for p in parts)  # whole bands per period
+
+
+def test_multi_plan_rejects_bad_arguments():
+    from raytrace2_amd._native import Rt2Error, multi_plan
+    assert multi_plan(4, [2, 2, 2, 2])[1]  # one GPU listed n times: loopback (tests' configuration)
+    assert not multi_plan(1, [5])[1]
+    for args in [(0, None), (3, [0, 1, 1]), (2, [0, -1]), (2, [0, 1], -1)]:
+        with pytest.raises(Rt2Error):
+            multi_plan(*args)
