@@ -242,6 +242,9 @@ typedef struct {
   double enqueue_ms;
   uint64_t readbacks;
   double readback_ms;
+  /* times the library blocked the host on the GPU (stream / event synchronizations); the launch path
+   * (Render, flush, gather, the async readbacks) adds none */
+  uint64_t host_waits;
 } rt2_stats;
 RT2_API int rt2_tracer_get_stats(rt2_tracer* tr, rt2_stats* out);
 /* The stats of GPU `part` of a multi-GPU tracer (part 0 of a one-GPU tracer is itself). */

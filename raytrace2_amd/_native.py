@@ -61,7 +61,8 @@ class Stats(ctypes.Structure):
                                                                            ("gather_ms", ctypes.c_double),
                                                                            ("enqueue_ms", ctypes.c_double),
                                                                            ("readbacks", ctypes.c_uint64),
-                                                                           ("readback_ms", ctypes.c_double)]
+                                                                           ("readback_ms", ctypes.c_double),
+                                                                           ("host_waits", ctypes.c_uint64)]
 
     def as_dict(self):
         d = {n: (getattr(self, n) if n.endswith("_ms") else int(getattr(self, n))) for n, _ in self._fields_

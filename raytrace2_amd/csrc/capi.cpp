@@ -139,6 +139,7 @@ struct rt2_tracer {
   double readback_ms = 0;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> rpending;  // async readbacks' timing events
   double enqueue_ms = 0;  // host time spent enqueueing this tracer's renders (LaunchFrames)
+  uint64_t host_waits = 0;  // times the library blocked the host on this GPU (stream / event syncs, sync copies)
 };
 
 namespace {
@@ -252,6 +253,7 @@ hipEvent_t TakeEvent(rt2_tracer* t) {
 }
 
 int DrainEvents(rt2_tracer* t) {
+  if (!t->pending.empty() || !t->gpending.empty() || !t->rpending.empty()) t->host_waits++;
   for (auto& pr : t->pending) {
     HIP_TRY(hipEventSynchronize(pr.second));
     float ms = 0;
@@ -294,6 +296,7 @@ int Sync(rt2_tracer* t) {
   int rc = Flush(t);
   if (rc != RT2_OK) return rc;
   HIP_TRY(hipSetDevice(t->device));
+  t->host_waits++;
   HIP_TRY(hipStreamSynchronize(t->stream));
   return DrainEvents(t);
 }
@@ -1461,11 +1464,14 @@ int rt2_tracer_get_stats(rt2_tracer* t, rt2_stats* o) {
       sum.enqueue_ms += s.enqueue_ms;
       sum.readbacks += s.readbacks;
       sum.readback_ms += s.readback_ms;
+      sum.host_waits += s.host_waits;
     }
     *o = sum;
     return RT2_OK;
   }
+  const uint64_t waits = t->host_waits;  // (this diagnostic's own synchronization is not counted)
   int rc = Sync(t);
+  t->host_waits = waits;
   if (rc != RT2_OK) return rc;
   unsigned long long s[kStatsSlots];
   HIP_TRY(hipSetDevice(t->device));
@@ -1488,6 +1494,7 @@ int rt2_tracer_get_stats(rt2_tracer* t, rt2_stats* o) {
   o->enqueue_ms = t->enqueue_ms;
   o->readbacks = t->readbacks;
   o->readback_ms = t->readback_ms;
+  o->host_waits = t->host_waits;
   return RT2_OK;
 }
 
@@ -1679,6 +1686,7 @@ int rt2_tracer_reset_stats(rt2_tracer* t) {
   t->enqueue_ms = 0;
   t->readbacks = 0;
   t->readback_ms = 0;
+  t->host_waits = 0;
   return RT2_OK;
 }
 

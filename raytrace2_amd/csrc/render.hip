@@ -51,7 +51,8 @@ constexpr int kBlock = 256;
 #ifndef RT2_EXP_TWICE
 #define RT2_EXP_TWICE 0  // cost probes (bits): 1 resolve_hit, 2 rand_unit_vec3, 4 camera_ray, 8 slab test,
                          // 16 quad-run test, 32 threaded medium step, 64 its log, 128 its two boundary
-                         // queries run twice
+                         // queries, 256 a Philox block (at every refill), 512 the sample store /
+                         // staging, 1024 the work-item decode run twice
 #endif
 #ifndef RT2_EXP_WAVESTEPS
 #define RT2_EXP_WAVESTEPS 0  // diagnostic build: per-wave linear-traversal step counts into diag slots
@@ -441,6 +442,16 @@ struct PathT {
       if (fresh || i + (uint32_t)K > 4u) {
         uint32_t w0, w1, w2, w3;
         block((n >> 2) + (fresh ? 0u : 1u), w0, w1, w2, w3);
+#if RT2_EXP_TWICE & 256
+        {
+          uint32_t q0, q1, q2, q3, fr = frame;
+          asm volatile("" : "+v"(fr));
+          uint32_t key0, key1;
+          seed_args(key0, key1);
+          philox(key0, key1, pix, fr, (n >> 2) + 7u, q0, q1, q2, q3);
+          asm volatile("" ::"v"(q0), "v"(q1), "v"(q2), "v"(q3));
+        }
+#endif
 #pragma unroll
         for (int j = 0; j < K; j++)
           if (fresh || i + (uint32_t)j >= 4u) v[j] = sel4((i + (uint32_t)j) & 3u, w0, w1, w2, w3);
@@ -2128,6 +2139,10 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
       const uint32_t slot = fr & (kOctet - 1u);
       float* blk = A.samples() + 3ull * kOctet * ((unsigned long long)(fr / kOctet) * A.local_pixels() + lidx);
       const bool more = ((dl >> 16) & kChunkLeftMask) != 0u;  // frames of the chunk after this one
+#if RT2_EXP_TWICE & 512
+      for (int rep2 = 0; rep2 < 2; rep2++) {
+        asm volatile("" : "+v"(color.x), "+v"(color.y), "+v"(color.z));
+#endif
       if constexpr (kGroup != 0u) {
         lds_f32* oct = (lds_f32*)(lp + 64u * kOctP);
         const uint32_t gs = slot & (kGroup - 1u);  // slot within the group = LDS slot
@@ -2161,6 +2176,9 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
         blk[3u * slot + 1u] = color.y;
         blk[3u * slot + 2u] = color.z;
       }
+#if RT2_EXP_TWICE & 512
+      }
+#endif
       int f = (int)path.frame + 1;
       if (more) {
         path.start((uint32_t)f);

@@ -1,6 +1,8 @@
-"""Multi-GPU plumbing: interleaved row-band partition of the framebuffer and the gather of every
-rank's bands to rank 0 (one process per GPU, torch.distributed; RCCL over xGMI on MI355X, gloo in
-the CPU tests).
+"""Multi-GPU plumbing for callers that move the band stacks themselves: the interleaved row-band
+partition of the framebuffer and a torch.distributed gather of every rank's bands to rank 0 (RCCL
+over xGMI with device tensors on MI355X, gloo with host tensors in the CPU tests). The product's own
+gather is rt2_tracer_gather in librt2.so (ncclGather + the root's de-interleave kernel); this module
+is the same layout in torch terms.
 
 The render itself needs no communication: pixels are independent (RayTracer.cpp:62-69) and the
 sample streams are keyed by (seed, global pixel, frame), so the gathered image is bit-identical to
@@ -34,11 +36,21 @@ def deinterleave(stacks: np.ndarray, height: int, band_h: int) -> np.ndarray:
     return out
 
 
+def source_rows(height: int, band_h: int, world: int) -> np.ndarray:
+    """Image row y -> row of the rank-major padded stacks viewed as (world * max_rows) rows: the C
+    ABI's host de-interleave applied to the stacks' own row numbers (one channel)."""
+    max_rows = band_rows_max(height, band_h, world)
+    ids = np.arange(world * max_rows, dtype=np.float32).reshape(world, max_rows, 1, 1)
+    return deinterleave(ids, height, band_h)[:, 0, 0].astype(np.int64)
+
+
 class BandGather:
     """Gathers (rows_r, W, C) float32 band stacks of every rank into one (H, W, C) image on rank 0:
     every rank sends its padded stack (band_rows_max rows) with one torch.distributed gather into a
-    rank-major buffer, which rank 0 de-interleaves with the C ABI's layout code (the buffer ncclGather
-    fills inside rt2_tracer_gather has the same layout)."""
+    rank-major buffer (the layout ncclGather fills inside rt2_tracer_gather), which rank 0
+    de-interleaves with one index_select on the buffer's device by the C ABI's row map
+    (source_rows). The image stays where the stacks are: a device tensor for device buffers (no host
+    copy), a host tensor for CPU ones."""
 
     def __init__(self, height: int, width: int, band_h: int, world: int, rank: int, device: torch.device,
                  channels: int = 3, group: Optional[dist.ProcessGroup] = None):
@@ -51,14 +63,16 @@ class BandGather:
         self.image: Optional[torch.Tensor] = None
         if rank == 0:
             self.stacks = torch.zeros((world, self.max_rows, width, channels), dtype=torch.float32, device=device)
-            self.image = torch.zeros((height, width, channels), dtype=torch.float32)
+            self.image = torch.zeros((height, width, channels), dtype=torch.float32, device=device)
+            self.src = torch.from_numpy(source_rows(height, band_h, world)).to(device)
 
     def local_view(self) -> torch.Tensor:
         """The part of the send buffer this rank fills (its local rows)."""
         return self.send[:len(self.rows[self.rank])]
 
     def gather(self) -> Optional[torch.Tensor]:
-        """Collective: every rank calls it; rank 0 returns the assembled image (host), others None."""
+        """Collective: every rank calls it; rank 0 returns the assembled image (on the stacks' device),
+        the others None."""
         if self.world == 1:
             self.stacks[0].copy_(self.send)
         else:
@@ -66,6 +80,6 @@ class BandGather:
             dist.gather(self.send, recv, dst=0, group=self.group)
             if self.rank != 0:
                 return None
-        img = deinterleave(self.stacks.cpu().numpy(), self.height, self.band_h)
-        self.image.copy_(torch.from_numpy(img))
+        flat = self.stacks.view(self.world * self.max_rows, self.width, -1)
+        torch.index_select(flat, 0, self.src, out=self.image)
         return self.image

