@@ -80,7 +80,7 @@ struct rt2_tracer {
   uint8_t* d_pixels = nullptr;
   uint32_t* d_ray_counts = nullptr;
   bool ray_counts_on = false;
-  uint32_t* d_work = nullptr;
+  uint32_t* d_work = nullptr;  // one work counter per launch slot (words 0 and 16)
   unsigned long long* d_stats = nullptr;
   bool stats_on = false;
   int64_t frame_idx = 0;  // frames launched (FrameIdx() = frame_idx + queued)
@@ -89,10 +89,26 @@ struct rt2_tracer {
   int max_depth = 50;
   uint64_t seed = 0x5EED2024ull;
   int launch_frames = 0;
-  // per-frame sample buffer ([frames][local pixels] float3) that lets a pixel's frames be split
-  // into chunks rendered by different lanes and still be summed in frame order
-  float* d_samples = nullptr;
-  size_t samples_bytes = 0;
+  // Launch slots: a render launch runs on one of two render streams with that slot's per-frame
+  // sample buffer ([frames][local pixels] float3, which lets a pixel's frames be split into chunks
+  // rendered by different lanes and still be summed in frame order), chunk table and work counter;
+  // its accumulate_kernel runs on the tracer's stream after it. Consecutive launches alternate
+  // slots, so a launch does not wait for the previous one: its waves take the CUs the previous
+  // launch's tail leaves idle (LaunchFrames).
+  struct Slot {
+    hipStream_t stream = nullptr;
+    float* samples = nullptr;
+    size_t samples_bytes = 0;
+    uint32_t* chunks = nullptr;         // this slot's chunk table (ChunkSchedule)
+    size_t chunks_bytes = 0;
+    std::vector<uint32_t> chunks_host;  // what `chunks` holds (renders repeat one schedule: no upload)
+    hipEvent_t rendered = nullptr;      // the slot's last render launch finished (tracer stream waits)
+    hipEvent_t consumed = nullptr;      // the accumulate that last read `samples` finished
+    bool consumed_set = false;
+  };
+  Slot slots[2];
+  int next_slot = 0;
+  bool pipeline = true;  // RT2_PIPELINE=0: every launch waits for the tracer stream (no overlap)
   size_t sample_budget = size_t(16) << 30;  // bytes; bounds the frames per launch
   int work_split = 16;                     // chunk schedule: work left split into >= k items per lane (0: one chunk)
   int chunk_max = 64;                      // longest chunk (frames)
@@ -100,9 +116,6 @@ struct rt2_tracer {
   bool frame_tiles = false;                // this launch: items = one pixel x 64 short chunks per wave
   int frame_tile_len = 8;                  // most frames per chunk in frame-tile mode (RT2_FRAME_TILE_LEN)
   bool chunk_align = true;                 // chunks of >= kOctet frames: multiples of 4 frames
-  uint32_t* d_chunks = nullptr;            // chunk tables of the last render's launches (ChunkSchedule)
-  size_t chunks_bytes = 0;
-  std::vector<uint32_t> chunks_host;       // what d_chunks holds (renders repeat one schedule: no upload)
   struct Staging {                         // pinned host copies of uploaded tables, reusable once copied
     uint32_t* p;
     size_t bytes;
@@ -205,9 +218,11 @@ void FreeImage(rt2_tracer* t) {
 }
 
 void FreeFrame(rt2_tracer* t) {
-  if (t->d_samples) (void)hipFreeAsync(t->d_samples, t->stream);  // stream-ordered (LaunchFrames)
-  t->d_samples = nullptr;
-  t->samples_bytes = 0;
+  for (auto& sl : t->slots) {
+    if (sl.samples) (void)hipFreeAsync(sl.samples, sl.stream);  // stream-ordered (LaunchFrames)
+    sl.samples = nullptr;
+    sl.samples_bytes = 0;
+  }
   (void)hipFree(t->d_accum);
   (void)hipFree(t->d_pixels);
   (void)hipFree(t->d_ray_counts);
@@ -517,6 +532,12 @@ int rt2_tracer_create(const rt2_scene* s, int device, rt2_tracer** out) {
   HIP_TRY(hipSetDevice(device));
   HIP_TRY(hipStreamCreateWithFlags(&t->own_stream, hipStreamNonBlocking));
   t->stream = t->own_stream;
+  for (auto& sl : t->slots) {
+    HIP_TRY(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&sl.rendered, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&sl.consumed, hipEventDisableTiming));
+  }
+  if (const char* e = getenv("RT2_PIPELINE")) t->pipeline = e[0] != '0';
   const CompiledScene& c = s->compiled;
   int rc;
   if ((rc = Upload(&t->d_nodes, c.nodes.data(), c.nodes.size() * sizeof(float))) != RT2_OK) return rc;
@@ -532,7 +553,7 @@ int rt2_tracer_create(const rt2_scene* s, int device, rt2_tracer** out) {
     if ((rc = Upload(&t->d_lind, c.lind.data(), c.lind.size() * sizeof(float))) != RT2_OK) return rc;
     t->lin_len = (uint32_t)(c.lin.size() / 4);
   }
-  HIP_TRY(hipMalloc(&t->d_work, 64));
+  HIP_TRY(hipMalloc(&t->d_work, 128));
   HIP_TRY(hipMalloc(&t->d_stats, kStatsSlots * sizeof(unsigned long long)));
   HIP_TRY(hipMemset(t->d_stats, 0, kStatsSlots * sizeof(unsigned long long)));
   t->root = c.root;
@@ -602,13 +623,21 @@ void rt2_tracer_destroy(rt2_tracer* t) {
   (void)hipFree(t->d_lind);
   (void)hipFree(t->d_work);
   (void)hipFree(t->d_stats);
-  if (t->d_chunks) (void)hipFreeAsync(t->d_chunks, t->stream);
+  for (auto& sl : t->slots) {
+    if (sl.chunks) (void)hipFreeAsync(sl.chunks, sl.stream);
+    if (sl.stream) (void)hipStreamSynchronize(sl.stream);
+  }
   if (t->stream) (void)hipStreamSynchronize(t->stream);
   for (auto& st : t->staging) {
     (void)hipEventDestroy(st.done);
     (void)hipHostFree(st.p);
   }
   if (t->own_stream) (void)hipStreamDestroy(t->own_stream);
+  for (auto& sl : t->slots) {
+    if (sl.rendered) (void)hipEventDestroy(sl.rendered);
+    if (sl.consumed) (void)hipEventDestroy(sl.consumed);
+    if (sl.stream) (void)hipStreamDestroy(sl.stream);
+  }
   delete t;
 }
 
@@ -856,23 +885,24 @@ void ChunkSchedule(const rt2_tracer* t, int fb, int n, uint32_t tile_items, int6
   *first_len = first;
 }
 
-// Puts a render's chunk tables in d_chunks, ordered on the tracer's stream: the copy runs after the
-// launches already queued there (which may still read the old tables), from pinned staging memory,
-// so the host never waits for the GPU (a multi-GPU tracer enqueues every GPU's launches at once).
-// A render repeating the last schedule (the bench, a progressive loop's steady state) uploads nothing.
-int UploadChunks(rt2_tracer* t, const std::vector<uint32_t>& tab) {
-  if (t->d_chunks && tab == t->chunks_host) return RT2_OK;
+// Puts a launch's chunk table in its slot's table, ordered on the slot's render stream: the copy runs
+// after the launches already queued there (which may still read the old table), from pinned staging
+// memory, so the host never waits for the GPU (a multi-GPU tracer enqueues every GPU's launches at
+// once). A launch repeating the slot's last schedule (the bench, a progressive loop's steady state)
+// uploads nothing.
+int UploadChunks(rt2_tracer* t, rt2_tracer::Slot& sl, const std::vector<uint32_t>& tab) {
+  if (sl.chunks && tab == sl.chunks_host) return RT2_OK;
   const size_t bytes = tab.size() * sizeof(uint32_t);
-  if (bytes > t->chunks_bytes) {
+  if (bytes > sl.chunks_bytes) {
     // grow geometrically; stream-ordered free and allocation: the queued launches that read the old
-    // tables run first, and the host does not wait (hipFree would synchronize the device)
-    const size_t cap = std::max(bytes, 2 * t->chunks_bytes);
-    if (t->d_chunks) HIP_TRY(hipFreeAsync(t->d_chunks, t->stream));
-    t->d_chunks = nullptr;
-    t->chunks_bytes = 0;
-    t->chunks_host.clear();
-    HIP_TRY(hipMallocAsync((void**)&t->d_chunks, cap, t->stream));
-    t->chunks_bytes = cap;
+    // table run first, and the host does not wait (hipFree would synchronize the device)
+    const size_t cap = std::max(bytes, 2 * sl.chunks_bytes);
+    if (sl.chunks) HIP_TRY(hipFreeAsync(sl.chunks, sl.stream));
+    sl.chunks = nullptr;
+    sl.chunks_bytes = 0;
+    sl.chunks_host.clear();
+    HIP_TRY(hipMallocAsync((void**)&sl.chunks, cap, sl.stream));
+    sl.chunks_bytes = cap;
   }
   // a staging buffer whose previous copy has run, else a new one
   rt2_tracer::Staging* st = nullptr;
@@ -893,9 +923,9 @@ int UploadChunks(rt2_tracer* t, const std::vector<uint32_t>& tab) {
     st = &t->staging.back();
   }
   memcpy(st->p, tab.data(), bytes);
-  HIP_TRY(hipMemcpyAsync(t->d_chunks, st->p, bytes, hipMemcpyHostToDevice, t->stream));
-  HIP_TRY(hipEventRecord(st->done, t->stream));
-  t->chunks_host = tab;
+  HIP_TRY(hipMemcpyAsync(sl.chunks, st->p, bytes, hipMemcpyHostToDevice, sl.stream));
+  HIP_TRY(hipEventRecord(st->done, sl.stream));
+  sl.chunks_host = tab;
   return RT2_OK;
 }
 
@@ -1018,21 +1048,7 @@ int LaunchFrames(rt2_tracer* t, int n_frames) {
     per_launch = (int)std::min<size_t>((size_t)per_launch, groups * 64u);
   }
   const auto octets = [](size_t frames) { return (frames + kOctet - 1) / kOctet * kOctet; };
-  size_t need = octets((size_t)per_launch) * frame_bytes;
-  if (need > t->samples_bytes) {
-    // grow geometrically (progressive loops raise their frames per call a little at a time)
-    need = std::max(need, std::min(2 * t->samples_bytes, octets(budget_frames) * frame_bytes));
-    // stream-ordered: the queued launches still using the old buffer run first; the host does not
-    // wait (a multi-GPU tracer enqueues every GPU's render before any of them finishes)
-    if (t->d_samples) HIP_TRY(hipFreeAsync(t->d_samples, t->stream));
-    t->d_samples = nullptr;
-    t->samples_bytes = 0;
-    HIP_TRY(hipMallocAsync((void**)&t->d_samples, need, t->stream));
-    t->samples_bytes = need;
-  }
-  p.samples = t->d_samples;
   t->last_variant = variant;
-  // every launch's chunk table first (one stream-ordered upload), then the launches
   struct Launch {
     int frame_begin, n_frames, first_len;
     uint32_t n_chunks;
@@ -1052,12 +1068,42 @@ int LaunchFrames(rt2_tracer* t, int n_frames) {
     done += L.n_frames;
     fb += L.n_frames;
   }
-  int rc = UploadChunks(t, tabs);
-  if (rc != RT2_OK) return rc;
+  // The counting kernels add per-pixel ray counts that Reset() zeroes on the tracer stream: those
+  // launches wait for it, as every launch does with RT2_PIPELINE=0.
+  const bool serial = !t->pipeline || counting;
   for (const Launch& L : launches) {
+    rt2_tracer::Slot& sl = t->slots[t->next_slot];
+    t->next_slot ^= 1;
+    // the slot's render stream waits for the accumulate that last read its sample buffer (or, serial,
+    // for everything queued on the tracer stream so far); never for the other slot's render
+    if (serial) {
+      hipEvent_t e = TakeEvent(t);
+      if (!e) return Fail(RT2_ERR_HIP, "event create failed");
+      HIP_TRY(hipEventRecord(e, t->stream));
+      HIP_TRY(hipStreamWaitEvent(sl.stream, e, 0));
+      t->event_pool.push_back(e);
+    } else if (sl.consumed_set) {
+      HIP_TRY(hipStreamWaitEvent(sl.stream, sl.consumed, 0));
+    }
+    size_t need = octets((size_t)L.n_frames) * frame_bytes;
+    if (need > sl.samples_bytes) {
+      // grow geometrically (progressive loops raise their frames per call a little at a time)
+      need = std::max(need, std::min(2 * sl.samples_bytes, octets((size_t)per_launch) * frame_bytes));
+      // stream-ordered: the queued work still using the old buffer runs first; the host does not
+      // wait (a multi-GPU tracer enqueues every GPU's render before any of them finishes)
+      if (sl.samples) HIP_TRY(hipFreeAsync(sl.samples, sl.stream));
+      sl.samples = nullptr;
+      sl.samples_bytes = 0;
+      HIP_TRY(hipMallocAsync((void**)&sl.samples, need, sl.stream));
+      sl.samples_bytes = need;
+    }
+    p.samples = sl.samples;
+    const std::vector<uint32_t> tab(tabs.begin() + (long)L.table, tabs.begin() + (long)L.table + 2 * (L.n_chunks + 1));
+    int rc = UploadChunks(t, sl, tab);
+    if (rc != RT2_OK) return rc;
     p.frame_begin = L.frame_begin;
     p.n_frames = L.n_frames;
-    p.chunks = t->d_chunks + L.table;
+    p.chunks = sl.chunks;
     p.n_chunks = L.n_chunks;
     p.div_width = MakeMagic((uint32_t)t->width);  // pixel index -> (x, y)
     if (t->frame_tiles) {
@@ -1074,14 +1120,20 @@ int LaunchFrames(rt2_tracer* t, int n_frames) {
     grid = std::max(grid, 1);
     t->last_grid = grid;
     t->last_chunk_frames = L.first_len;
-    HIP_TRY(hipMemsetAsync(t->d_work, 0, sizeof(uint32_t), t->stream));
+    p.work_counter = t->d_work + 16 * (&sl - t->slots);
+    HIP_TRY(hipMemsetAsync(p.work_counter, 0, sizeof(uint32_t), sl.stream));
     hipEvent_t e0 = TakeEvent(t), e1 = TakeEvent(t);
-    if (e0) HIP_TRY(hipEventRecord(e0, t->stream));
-    HIP_TRY(LaunchRender(p, variant, counting, grid, t->stream));
-    if (e1) HIP_TRY(hipEventRecord(e1, t->stream));
+    if (e0) HIP_TRY(hipEventRecord(e0, sl.stream));
+    HIP_TRY(LaunchRender(p, variant, counting, grid, sl.stream));
+    if (e1) HIP_TRY(hipEventRecord(e1, sl.stream));
     if (e0 && e1) t->pending.emplace_back(e0, e1);
-    HIP_TRY(LaunchAccumulate(t->d_samples, t->d_accum, t->d_pixels, p.local_pixels, p.n_frames,
+    // accumulate in frame order on the tracer stream, after this launch (RayTracer.cpp:64)
+    HIP_TRY(hipEventRecord(sl.rendered, sl.stream));
+    HIP_TRY(hipStreamWaitEvent(t->stream, sl.rendered, 0));
+    HIP_TRY(LaunchAccumulate(sl.samples, t->d_accum, t->d_pixels, p.local_pixels, p.n_frames,
                              p.frame_begin + p.n_frames, t->stream));
+    HIP_TRY(hipEventRecord(sl.consumed, t->stream));
+    sl.consumed_set = true;
     t->launches++;
     t->paths += (uint64_t)p.n_frames * p.local_pixels;
     t->frame_idx += p.n_frames;

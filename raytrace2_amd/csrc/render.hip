@@ -86,6 +86,9 @@ constexpr int kBlock = 256;
 #ifndef RT2_PARK
 #define RT2_PARK 1
 #endif
+#ifndef RT2_RNG_RING
+#define RT2_RNG_RING 1
+#endif
 #ifndef RT2_KEEP_WINV
 #define RT2_KEEP_WINV 1
 #endif
@@ -411,28 +414,81 @@ typedef __attribute__((address_space(3))) float lds_f32;
 
 // The per-lane path context the samplers need. kLdsRng: the lane's current Philox block lives in
 // four LDS planes (word k at rb[64 k]) instead of four VGPRs that stay live across the whole render
-// loop.
-template <bool kLdsRng>
+// loop. kRing: eight planes hold two consecutive blocks (draw j at rb[64 (j & 7)]), so the next block
+// can be computed before the current one is used up: the render loop computes, in ONE place per
+// bounce, the block each lane will draw from next (prefetch: a scattering lane's next block, or
+// block 0 of the next frame for a lane starting its next path). Without it the wave runs the Philox
+// code at every draw site where any lane refills: the scatter site and the camera site of the
+// lanes that start a path, both in nearly every bounce (profiles/r04_c2_cost_probes.json). The
+// draws are the same values in the same order.
+template <bool kLdsRng, bool kRing = false>
 struct PathT {
   static constexpr bool kLds = kLdsRng;
   uint32_t frame;
   uint32_t pix;  // global pixel index y * width + x (the stream's pixel word)
   uint32_t sij;  // stratum s_i | s_j << 16 of `frame` (RayTracer.cpp:59-60), advanced per frame
-  uint32_t n;
+  uint32_t n;    // draws taken in this frame; kRing: | (draws loaded and not taken) << 28
   uint32_t r0, r1, r2, r3;  // the block (kLdsRng false)
   lds_u32* rb;              // the lane's Philox planes (kLdsRng true)
   __device__ __forceinline__ void start(uint32_t f) {
     frame = f;
     n = 0;  // buffer holds block -1: the first group refills
   }
+  // kRing: the next frame's block 0 is already in the ring (prefetch with restart)
+  __device__ __forceinline__ void start_loaded(uint32_t f) {
+    frame = f;
+    n = 4u << 28;
+  }
   __device__ __forceinline__ void block(uint32_t b, uint32_t& w0, uint32_t& w1, uint32_t& w2, uint32_t& w3) const {
     uint32_t key0, key1;
     seed_args(key0, key1);  // re-read at the refill (see karg16)
     philox(key0, key1, pix, frame, b, w0, w1, w2, w3);
   }
+  // kRing: block b of frame f into the ring (half b & 1)
+  __device__ __forceinline__ void ring_put(uint32_t f, uint32_t b) {
+    uint32_t key0, key1, w0, w1, w2, w3;
+    seed_args(key0, key1);
+    philox(key0, key1, pix, f, b, w0, w1, w2, w3);
+#if RT2_EXP_TWICE & 256
+    {
+      uint32_t q0, q1, q2, q3, fr = f;
+      asm volatile("" : "+v"(fr));
+      philox(key0, key1, pix, fr, b + 7u, q0, q1, q2, q3);
+      asm volatile("" ::"v"(q0), "v"(q1), "v"(q2), "v"(q3));
+    }
+#endif
+    lds_u32* h = rb + 256u * (b & 1u);
+    h[0] = w0;
+    h[64] = w1;
+    h[128] = w2;
+    h[192] = w3;
+  }
+  // kRing: the one refill site of a bounce. scatter: the lane will take up to 2 draws of this frame;
+  // restart: the lane's path is done and its next frame starts (block 0 of frame + 1).
+  __device__ __forceinline__ void prefetch(bool scatter, bool restart) {
+    const uint32_t nn = n & 0x0FFFFFFFu, ah = n >> 28;
+    const bool more = scatter && ah < 2u;
+    if (more || restart) {
+      ring_put(restart ? frame + 1u : frame, restart ? 0u : (nn + ah) >> 2);
+      if (more) n += 4u << 28;
+    }
+  }
   // K consecutive uniforms in [0,1) (24-bit mantissa), in stream order
   template <int K>
   __device__ __forceinline__ void take(float* out) {
+    if constexpr (kRing) {
+      static_assert(kLdsRng && K <= 4, "ring draws");
+      const uint32_t nn = n & 0x0FFFFFFFu;
+      uint32_t ah = n >> 28;
+      if (ah < (uint32_t)K) {  // not prefetched (a path's first camera ray after a work fetch)
+        ring_put(frame, (nn + ah) >> 2);
+        ah += 4u;
+      }
+#pragma unroll
+      for (int j = 0; j < K; j++) out[j] = to_unit(rb[64u * ((nn + (uint32_t)j) & 7u)]);
+      n = (nn + (uint32_t)K) | ((ah - (uint32_t)K) << 28);
+      return;
+    }
     uint32_t i = n & 3u;
     bool fresh = i == 0u;
     uint32_t v[K];
@@ -1170,6 +1226,14 @@ __device__ __forceinline__ bool medium_t_lin(const void* recs, uint32_t moff, co
   return true;
 }
 
+// The closest hit's world-space record and its material (resolve_hit + the material table)
+struct HitShade {
+  f3 hp, hn;
+  bool front;
+  float4 m0, m1;
+  uint32_t type;
+};
+
 struct HitRef {
   float t;
   uint32_t prim;  // ref of the quad / sphere / medium that produced the closest hit
@@ -1857,7 +1921,9 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
   constexpr bool kLdsRng = LdsRng<F, kMode, kStats>();
   constexpr bool kPark = Park<F, kMode, kStats>();
   // the wave's LDS planes (lds_u32): Philox block, sample staging, box-boundary candidates, parked path
-  constexpr uint32_t kRngP = 0u, kOctP = kRngP + (kLdsRng ? 4u : 0u), kCandP = kOctP + (kGroup ? kPlanes : 0u);
+  constexpr uint32_t kRngP = 0u,
+                     kOctP = kRngP + (kLdsRng ? ((RT2_RNG_RING && !kPark && !BoxPair<F, kMode>()) ? 8u : 4u) : 0u),
+                     kCandP = kOctP + (kGroup ? kPlanes : 0u);
   constexpr uint32_t kParkP = kCandP + (BoxPair<F, kMode>() ? kBoundaryAAMax : 0u);
   constexpr uint32_t kWavePlanes = kParkP + (kPark ? (uint32_t)kParkWords : 0u);
   lds_u32* lp = nullptr;  // this lane's word of plane 0
@@ -1872,7 +1938,10 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
   unsigned long long rays = 0;  // rays cast by the wave (popcounts of a ballot at the loop head)
   uint32_t bnext = 0, bend = 0;  // the wave's reserved batch of work items (wave-uniform)
   uint32_t item_rays = 0;
-  PathT<kLdsRng> path;
+  // two-block Philox ring where the LDS room allows it (8 planes instead of 4: not beside the Cornell
+  // volume kernel's candidate planes or book 2's park planes)
+  constexpr bool kRing = RT2_RNG_RING && kLdsRng && !kPark && !BoxPair<F, kMode>();
+  PathT<kLdsRng, kRing> path;
   path.rb = lp + 64u * kRngP;
   lds_u32* pk = lp + 64u * kParkP;  // this lane's park planes (kPark)
   path.pix = 0;
@@ -2008,51 +2077,11 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
     // ---- one bounce (RayColor, RayTracer.cpp:20-45)
     bool done = false;
     f3 color = mk(0, 0, 0);
-    if ((dl & 0xFFFFu) == 0u) {
-      done = true;  // RayColor(depth <= 0) returns 0 without casting a ray
-    } else {
-      if constexpr (kStats) item_rays++;
-      HitRef h;
-      bool hit;
-      if constexpr (kPark) {
-        pk_st3(pk, kPkThr, thr);
-        pk_st(pk, kPkDl, dl);
-        pk_st(pk, kPkSij, path.sij);
-        pk_st(pk, kPkFrame, path.frame);
-        pk_st(pk, kPkPix, path.pix);
-        pk_st(pk, kPkN, path.n);
-        pk_st3(pk, kPkO, ro);
-        pk_st3(pk, kPkD, rd);
-        ParkedPath pp{path.rb, pk};
-        hit = trace_linear<F, kStats>(P, ParkRay{pk}, rtime, pp, h, lp + 64u * kCandP, cnt);
-        thr = pk_ld3(pk, kPkThr);
-        dl = pk_ld(pk, kPkDl);
-        path.sij = pk_ld(pk, kPkSij);
-        path.frame = pk_ld(pk, kPkFrame);
-        path.pix = pk_ld(pk, kPkPix);
-        path.n = pk_ld(pk, kPkN);
-        ro = pk_ld3(pk, kPkO);
-        rd = pk_ld3(pk, kPkD);
-      } else if constexpr (kMode == kModeLinear) {
-        hit = trace_linear<F, kStats>(P, RegRay{ro, rd}, rtime, path, h, lp + 64u * kCandP, cnt);
-#if RT2_EXP_TRACE_TWICE
-        {
-          f3 ro2 = ro;
-          asm volatile("" : "+v"(ro2.x), "+v"(ro2.y), "+v"(ro2.z));
-          HitRef h2;
-          auto p2 = path;
-          bool hit2 = trace_linear<F, kStats>(P, RegRay{ro2, rd}, rtime, p2, h2, lp + 64u * kCandP, cnt);
-          asm volatile("" ::"v"(h2.t), "v"(h2.prim), "v"(h2.xf), "v"((int)hit2));
-        }
-#endif
-      } else {
-        hit = trace_stack<F, kMode, kStats>(P, N, ro, rd, rtime, path, h, stk, cnt, overflow);
-      }
-      RT2_STAMP(st_trace);
-      if (!hit) {
-        color = thr * bg;
-        done = true;
-      } else {
+    HitRef h;
+    bool hit = false;
+    // the closest hit's record and material, then its emission or scatter (RayColor,
+    // RayTracer.cpp:26-44)
+    auto resolve = [&](const ShadeArgs& S) {
         f3 hp, hn;
         bool front;
         uint32_t mat;
@@ -2074,9 +2103,14 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
         } else {
           resolve_hit<F>(N, h, ro, rd, rtime, hp, hn, front, mat);
         }
-        const ShadeArgs S = shade_args();
-        float4 m0 = S.materials[2 * mat], m1 = S.materials[2 * mat + 1];
-        uint32_t type = bits(m0.x);
+        const float4 m0 = S.materials[2 * mat], m1 = S.materials[2 * mat + 1];
+        return HitShade{hp, hn, front, m0, m1, bits(m0.x)};
+    };
+    auto shade = [&](const HitShade& hs, const ShadeArgs& S) {
+        const f3 hp = hs.hp, hn = hs.hn;
+        const bool front = hs.front;
+        const float4 m0 = hs.m0, m1 = hs.m1;
+        const uint32_t type = hs.type;
         if (type == kMatDiffuseLight) {
           color = thr * tex_value<F>(S, bits(m1.z), hp);
           done = true;
@@ -2125,6 +2159,72 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
           ro = hp;
           rd = dir;
           dl--;  // depth_left > 0 here: no borrow into the frame count
+        }
+    };
+    if ((dl & 0xFFFFu) == 0u) {
+      done = true;  // RayColor(depth <= 0) returns 0 without casting a ray
+    } else {
+      if constexpr (kStats) item_rays++;
+      if constexpr (kPark) {
+        pk_st3(pk, kPkThr, thr);
+        pk_st(pk, kPkDl, dl);
+        pk_st(pk, kPkSij, path.sij);
+        pk_st(pk, kPkFrame, path.frame);
+        pk_st(pk, kPkPix, path.pix);
+        pk_st(pk, kPkN, path.n);
+        pk_st3(pk, kPkO, ro);
+        pk_st3(pk, kPkD, rd);
+        ParkedPath pp{path.rb, pk};
+        hit = trace_linear<F, kStats>(P, ParkRay{pk}, rtime, pp, h, lp + 64u * kCandP, cnt);
+        thr = pk_ld3(pk, kPkThr);
+        dl = pk_ld(pk, kPkDl);
+        path.sij = pk_ld(pk, kPkSij);
+        path.frame = pk_ld(pk, kPkFrame);
+        path.pix = pk_ld(pk, kPkPix);
+        path.n = pk_ld(pk, kPkN);
+        ro = pk_ld3(pk, kPkO);
+        rd = pk_ld3(pk, kPkD);
+      } else if constexpr (kMode == kModeLinear) {
+        hit = trace_linear<F, kStats>(P, RegRay{ro, rd}, rtime, path, h, lp + 64u * kCandP, cnt);
+#if RT2_EXP_TRACE_TWICE
+        {
+          f3 ro2 = ro;
+          asm volatile("" : "+v"(ro2.x), "+v"(ro2.y), "+v"(ro2.z));
+          HitRef h2;
+          auto p2 = path;
+          bool hit2 = trace_linear<F, kStats>(P, RegRay{ro2, rd}, rtime, p2, h2, lp + 64u * kCandP, cnt);
+          asm volatile("" ::"v"(h2.t), "v"(h2.prim), "v"(h2.xf), "v"((int)hit2));
+        }
+#endif
+      } else {
+        hit = trace_stack<F, kMode, kStats>(P, N, ro, rd, rtime, path, h, stk, cnt, overflow);
+      }
+      RT2_STAMP(st_trace);
+      if constexpr (!kRing) {
+        if (!hit) {
+          color = thr * bg;
+          done = true;
+        } else {
+          const ShadeArgs S = shade_args();
+          shade(resolve(S), S);
+        }
+      }
+    }
+    if constexpr (kRing) {
+      // the hit lanes' records and materials first, so the bounce's one Philox site (PathT kRing)
+      // knows which lanes scatter and which start their next frame
+      HitShade hs{mk(0, 0, 0), mk(0, 0, 0), false, make_float4(0, 0, 0, 0), make_float4(0, 0, 0, 0),
+                  kMatDiffuseLight};
+      const ShadeArgs S = shade_args();
+      if (hit) hs = resolve(S);
+      const bool scatter = hit && hs.type != kMatDiffuseLight;
+      path.prefetch(scatter, !scatter && ((dl >> 16) & kChunkLeftMask) != 0u);
+      if (!done) {
+        if (!hit) {
+          color = thr * bg;
+          done = true;
+        } else {
+          shade(hs, S);
         }
       }
     }
@@ -2181,7 +2281,11 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
 #endif
       int f = (int)path.frame + 1;
       if (more) {
-        path.start((uint32_t)f);
+        if constexpr (kRing) {
+          path.start_loaded((uint32_t)f);  // its block 0 came with the bounce's prefetch
+        } else {
+          path.start((uint32_t)f);
+        }
         {  // next stratum: (f % sq, f / sq % sq) from the previous frame's
           const uint32_t sq = (uint32_t)P.cam.sqrt_spp;
           uint32_t si = (path.sij & 0xFFFFu) + 1u, sj = path.sij >> 16;
