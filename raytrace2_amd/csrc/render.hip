@@ -86,6 +86,12 @@ constexpr int kBlock = 256;
 #ifndef RT2_PARK
 #define RT2_PARK 1
 #endif
+#ifndef RT2_STAGE
+#define RT2_STAGE 1  // 0: samples written with plain 12-B stores (no LDS staging)
+#endif
+#ifndef RT2_STAGE_RING
+#define RT2_STAGE_RING 0  // 1: the ring kernels stage samples in LDS too
+#endif
 #ifndef RT2_RNG_RING
 #define RT2_RNG_RING 1
 #endif
@@ -1891,18 +1897,28 @@ constexpr bool Park() {
   constexpr uint32_t kBook2 = kFeatSphere | kFeatMedium | kFeatXform | kFeatNoise | kFeatSpecular | kFeatAccList;
   return RT2_PARK && F == kBook2 && kMode == kModeLinear && !kStats && LdsRng<F, kMode, kStats>();
 }
-template <uint32_t F, int kMode, bool kStats>
-constexpr uint32_t StageGroup() {
-  if (kMode != kModeLinear || kStats || Park<F, kMode, kStats>()) return 0u;
-  // octets need 5.25 KB per wave: with the LDS Philox blocks beside them they fit no occupancy >= 7
-  return MinWaves<F, kMode, kStats>() <= 7 && !LdsRng<F, kMode, kStats>() ? 8u : 4u;
-}
-
 // Kernels whose threaded medium step takes both box-boundary queries in one pass (boundary_aa_pair):
 // their LDS holds the candidates.
 template <uint32_t F, int kMode>
 constexpr bool BoxPair() {
   return RT2_BOX_PAIR && kMode == kModeLinear && Has<F, kFeatMedium>() && !Has<F, kFeatSphere>();
+}
+
+// Kernels with the two-block Philox ring (PathT kRing): 8 Philox planes, where the LDS room allows it (not
+// beside the Cornell volume kernel's candidate planes or book 2's park planes).
+template <uint32_t F, int kMode, bool kStats>
+constexpr bool Ring() {
+  return RT2_RNG_RING && LdsRng<F, kMode, kStats>() && !Park<F, kMode, kStats>() && !BoxPair<F, kMode>();
+}
+template <uint32_t F, int kMode, bool kStats>
+constexpr uint32_t StageGroup() {
+  if (kMode != kModeLinear || kStats || Park<F, kMode, kStats>()) return 0u;
+  // the ring kernels (Cornell, book 1) store samples directly: their staging logic cost more time than
+  // the write traffic it saves (round 4, same box: C2 +0.9 %, book 1 +1 %; 12-B stores write the
+  // octets' sectors partially, about 3x the sample bytes, 2.5 % of HBM bandwidth at the headline)
+  if (!RT2_STAGE || (RT2_STAGE_RING == 0 && Ring<F, kMode, kStats>())) return 0u;
+  // octets need 5.25 KB per wave: with the LDS Philox blocks beside them they fit no occupancy >= 7
+  return MinWaves<F, kMode, kStats>() <= 7 && !LdsRng<F, kMode, kStats>() ? 8u : 4u;
 }
 
 template <uint32_t F, int kMode, bool kStats>
@@ -1922,7 +1938,7 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
   constexpr bool kPark = Park<F, kMode, kStats>();
   // the wave's LDS planes (lds_u32): Philox block, sample staging, box-boundary candidates, parked path
   constexpr uint32_t kRngP = 0u,
-                     kOctP = kRngP + (kLdsRng ? ((RT2_RNG_RING && !kPark && !BoxPair<F, kMode>()) ? 8u : 4u) : 0u),
+                     kOctP = kRngP + (kLdsRng ? (Ring<F, kMode, kStats>() ? 8u : 4u) : 0u),
                      kCandP = kOctP + (kGroup ? kPlanes : 0u);
   constexpr uint32_t kParkP = kCandP + (BoxPair<F, kMode>() ? kBoundaryAAMax : 0u);
   constexpr uint32_t kWavePlanes = kParkP + (kPark ? (uint32_t)kParkWords : 0u);
@@ -1938,9 +1954,7 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
   unsigned long long rays = 0;  // rays cast by the wave (popcounts of a ballot at the loop head)
   uint32_t bnext = 0, bend = 0;  // the wave's reserved batch of work items (wave-uniform)
   uint32_t item_rays = 0;
-  // two-block Philox ring where the LDS room allows it (8 planes instead of 4: not beside the Cornell
-  // volume kernel's candidate planes or book 2's park planes)
-  constexpr bool kRing = RT2_RNG_RING && kLdsRng && !kPark && !BoxPair<F, kMode>();
+  constexpr bool kRing = Ring<F, kMode, kStats>();  // two-block Philox ring
   PathT<kLdsRng, kRing> path;
   path.rb = lp + 64u * kRngP;
   lds_u32* pk = lp + 64u * kParkP;  // this lane's park planes (kPark)

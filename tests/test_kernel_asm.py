@@ -68,3 +68,43 @@ def test_no_scratch_in_bench_variants(isa):
         stores = [m.start() for m in re.finditer(r"scratch_store|buffer_store.*Spill", body)]
         assert head is not None and all(p < head.start() for p in stores), (name, len(stores))
     assert seen == 1
+
+
+def _loop_depth_scratch(body):
+    """(loop depth, instruction) of every scratch (spill) access in a kernel body."""
+    out, depth = [], 0
+    for line in body.split("\n"):
+        if line.startswith(".LBB") or line.startswith("; %bb"):
+            m = re.search(r"Depth=(\d+)", line)
+            depth = int(m.group(1)) if m else 0
+        t = line.strip()
+        if t.startswith("scratch_"):
+            out.append((depth, t.split()[0]))
+    return out
+
+
+def _kernel(isa, tag):
+    s, remarks = isa
+    blk = [b for b in re.split(r"remark: Function Name: ", remarks)[1:] if tag in b.split()[0]]
+    assert len(blk) == 1, tag
+    name = blk[0].split()[0]
+    scratch = int(re.search(r"ScratchSize \[bytes/lane\]: (\d+)", blk[0]).group(1))
+    body = s.split(f"\n{name}:", 1)[1].split(".Lfunc_end", 1)[0]
+    return scratch, body
+
+
+def test_no_scratch_in_cornell_volume_bench_kernel(isa):
+    """the Cornell volume kernel the C4 bench runs (threaded, 8 waves) must not spill to
+    scratch (round 3's one-pass box boundaries had pushed it to 25 spilled VGPRs, 56 B per lane)."""
+    scratch, body = _kernel(isa, "ILj6ELi2ELb0E")
+    assert scratch == 0 and not _loop_depth_scratch(body), (scratch, _loop_depth_scratch(body)[:5])
+
+
+def test_book2_bench_kernel_spills_stay_out_of_the_trace(isa):
+    """The book 2 kernel (C5) runs at 8 waves with VGPRs spilled (occupancy beats spills there, DESIGN
+    §4): its scratch stays at most 96 B per lane and no spill store or reload sits inside the trace's
+    loops (loop depth >= 2); the reloads left are the marble texture's double-precision sin constants
+    on the shading path (depth 1)."""
+    scratch, body = _kernel(isa, "ILj303ELi2ELb0E")
+    deep = [x for x in _loop_depth_scratch(body) if x[0] >= 2]
+    assert scratch <= 96 and not deep, (scratch, deep[:5])
