@@ -62,6 +62,7 @@ struct rt2_tracer {
   uint32_t features = 0;
   int max_stack = 1;
   bool stack_ok = true;  // the scene fits the stack traversal (else only the threaded program runs it)
+  bool flat_xforms = true;  // no nested transforms in the threaded program (RenderParams::flat_xforms)
   bool use_lds = true;
   bool use_hybrid = true;   // stage only the BVH prefix in LDS when the scene is too large
   bool force_hybrid = false;  // tests: hybrid even when the whole scene would fit
@@ -562,6 +563,7 @@ int rt2_tracer_create(const rt2_scene* s, int device, rt2_tracer** out) {
   t->features = c.features;
   t->max_stack = c.max_stack;
   t->stack_ok = c.stack_ok;
+  t->flat_xforms = c.lin_xform_depth <= 1;
   Put3(t->background, s->scene.background);
   t->camera = s->scene.cam;
   HIP_TRY(hipDeviceGetAttribute(&t->cus, hipDeviceAttributeMultiprocessorCount, device));
@@ -978,6 +980,7 @@ int LaunchFrames(rt2_tracer* t, int n_frames) {
   p.lin_wide = t->d_lin_wide;
   p.lind = t->d_lind;
   p.lin_len = t->use_linear ? t->lin_len : 0u;
+  p.flat_xforms = t->flat_xforms ? 1u : 0u;
   if (!p.lin_len && !t->stack_ok)
     return Fail(RT2_ERR_INVALID, "scene needs a traversal stack of " + std::to_string(t->max_stack) +
                                      " entries (kernel has " + std::to_string(kTraversalStack) +

@@ -464,9 +464,13 @@ struct Flattener {
         uint32_t self = make_ref(kXform, off);
         if (xf_depth >= kLinearMaxXformDepth) return false;  // the kernel nests one loop per level
         size_t me = emit(kXform, off, 0);
+        out.lin_xform_depth = std::max(out.lin_xform_depth, xf_depth + 1);
         if (!Linearize(o.child, self, lin, lind, xf_depth + 1)) return false;
         lin[4 * me + 1] = (uint32_t)(lin.size() / 4);  // index of the matching exit step
-        emit(kXformExit, off, parent_xf);
+        // exit step: skip = the end of the transform's record range [off + kXformRecords, end) (the
+        // records of every primitive under it follow its own record)
+        const size_t ex = emit(kXformExit, off, parent_xf);
+        lin[4 * ex + 1] = (uint32_t)(lind.size() / 4);
         return true;
       }
       case kMedium: {

@@ -89,6 +89,9 @@ constexpr int kBlock = 256;
 #ifndef RT2_STAGE
 #define RT2_STAGE 1  // 0: samples written with plain 12-B stores (no LDS staging)
 #endif
+#ifndef RT2_XRAY
+#define RT2_XRAY 1  // the Cornell kernel keeps the hit's model-space ray from the trace (resolve_hit)
+#endif
 #ifndef RT2_STAGE_RING
 #define RT2_STAGE_RING 0  // 1: the ring kernels stage samples in LDS too
 #endif
@@ -1415,7 +1418,7 @@ __device__ __forceinline__ uint32_t wave_min_next(uint32_t next) {
 
 template <uint32_t F, bool kStats, class W, class G>
 __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wray, float time, G& path, HitRef& h,
-                                             lds_u32* cand, Counters& cnt) {
+                                             lds_u32* cand, lds_u32* xray, Counters& cnt) {
   const Nodes<kModeLinear> N{reinterpret_cast<const float4*>(P.lind)};  // boundaries / nested xforms
   const void* recs = P.lind;
   // the world ray's reciprocal is recomputed where a transform's exit returns to world space
@@ -1573,6 +1576,13 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
       fin = finite3(inv);
       cur_xf = make_ref(kXform, off);
     } else if (Has<F, kFeatXform>() && kind == kXformExit) {
+      // kept model-space ray (xray planes, flat transforms): the closest primitive so far lies under
+      // this transform (its record in [off + 8, skip)), so this space's ray is what resolve_hit needs
+      if (xray != nullptr && P.flat_xforms != 0u && prim - make_ref(prim >> 28, off + (uint32_t)kXformRecords) <
+                                                       st.y - (off + (uint32_t)kXformRecords)) {
+        pk_st3(xray, 0u, o);
+        pk_st3(xray, 3u, d);
+      }
       cur_xf = st.w;
       if (cur_xf == kRefNone) {
         o = wray.wo();
@@ -1686,9 +1696,17 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
 // TransformedHittable::Hit returns): point, normal, front_face, material.
 template <uint32_t F, int kMode>
 __device__ __forceinline__ void resolve_hit(const Nodes<kMode>& N, const HitRef& h, f3 wo, f3 wd, float time, f3& p,
-                                            f3& n, bool& front, uint32_t& mat) {
+                                            f3& n, bool& front, uint32_t& mat, const lds_u32* xray = nullptr,
+                                            bool flat = false) {
   f3 o = wo, d = wd;
-  if constexpr (Has<F, kFeatXform>()) ray_in_space(N, h.xf, wo, wd, o, d);
+  if constexpr (Has<F, kFeatXform>()) {
+    if (xray != nullptr && flat && h.xf != kRefNone) {  // the trace kept the hit's model-space ray
+      o = pk_ld3(xray, 0u);
+      d = pk_ld3(xray, 3u);
+    } else {
+      ray_in_space(N, h.xf, wo, wd, o, d);
+    }
+  }
   uint32_t kind = h.prim >> 28, off = h.prim & kOffsetMask;
   p = o + d * h.t;
   if (Has<F, kFeatMedium>() && kind == kMedium) {
@@ -1941,7 +1959,11 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
                      kOctP = kRngP + (kLdsRng ? (Ring<F, kMode, kStats>() ? 8u : 4u) : 0u),
                      kCandP = kOctP + (kGroup ? kPlanes : 0u);
   constexpr uint32_t kParkP = kCandP + (BoxPair<F, kMode>() ? kBoundaryAAMax : 0u);
-  constexpr uint32_t kWavePlanes = kParkP + (kPark ? (uint32_t)kParkWords : 0u);
+  // the model-space ray of the transform holding the closest hit, kept by the trace for resolve_hit
+  // (the ring kernels with transforms: the Cornell box)
+  constexpr bool kXray = RT2_XRAY && Ring<F, kMode, kStats>() && Has<F, kFeatXform>();
+  constexpr uint32_t kXrayP = kParkP + (kPark ? (uint32_t)kParkWords : 0u);
+  constexpr uint32_t kWavePlanes = kXrayP + (kXray ? 6u : 0u);
   lds_u32* lp = nullptr;  // this lane's word of plane 0
   if constexpr (kWavePlanes != 0u) {
     __shared__ uint32_t s_planes[(kBlock / 64) * kWavePlanes * 64];
@@ -2101,7 +2123,7 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
         uint32_t mat;
         if constexpr (kMode == kModeLinear) {
           resolve_hit<F>(Nodes<kModeLinear>{reinterpret_cast<const float4*>(P.lind)}, h, ro, rd, rtime, hp, hn, front,
-                         mat);
+                         mat, kXray ? lp + 64u * kXrayP : nullptr, kXray && P.flat_xforms != 0u);
 #if RT2_EXP_TWICE & 1
           {
             f3 ro2 = ro, hp2, hn2;
@@ -2189,7 +2211,7 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
         pk_st3(pk, kPkO, ro);
         pk_st3(pk, kPkD, rd);
         ParkedPath pp{path.rb, pk};
-        hit = trace_linear<F, kStats>(P, ParkRay{pk}, rtime, pp, h, lp + 64u * kCandP, cnt);
+        hit = trace_linear<F, kStats>(P, ParkRay{pk}, rtime, pp, h, lp + 64u * kCandP, nullptr, cnt);
         thr = pk_ld3(pk, kPkThr);
         dl = pk_ld(pk, kPkDl);
         path.sij = pk_ld(pk, kPkSij);
@@ -2199,14 +2221,15 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
         ro = pk_ld3(pk, kPkO);
         rd = pk_ld3(pk, kPkD);
       } else if constexpr (kMode == kModeLinear) {
-        hit = trace_linear<F, kStats>(P, RegRay{ro, rd}, rtime, path, h, lp + 64u * kCandP, cnt);
+        hit = trace_linear<F, kStats>(P, RegRay{ro, rd}, rtime, path, h, lp + 64u * kCandP,
+                                      kXray ? lp + 64u * kXrayP : nullptr, cnt);
 #if RT2_EXP_TRACE_TWICE
         {
           f3 ro2 = ro;
           asm volatile("" : "+v"(ro2.x), "+v"(ro2.y), "+v"(ro2.z));
           HitRef h2;
           auto p2 = path;
-          bool hit2 = trace_linear<F, kStats>(P, RegRay{ro2, rd}, rtime, p2, h2, lp + 64u * kCandP, cnt);
+          bool hit2 = trace_linear<F, kStats>(P, RegRay{ro2, rd}, rtime, p2, h2, lp + 64u * kCandP, nullptr, cnt);
           asm volatile("" ::"v"(h2.t), "v"(h2.prim), "v"(h2.xf), "v"((int)hit2));
         }
 #endif

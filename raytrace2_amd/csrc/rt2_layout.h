@@ -154,7 +154,8 @@ constexpr int kLdsSceneBytesMax = 96 * 1024;  // scenes up to this size are stag
 //     (codes 4..6 use the QUADAA record layout, the others the QUAD layout)
 //   kind kXform: enter the transform (record = XFORM record, skip = index of its kXformExit);
 //     the kernel walks the steps up to the exit in a nested loop with the transformed ray
-//   kind kXformExit: leave it (record = XFORM record, aux = parent XFORM ref or kRefNone)
+//   kind kXformExit: leave it (record = XFORM record, aux = parent XFORM ref or kRefNone, skip = the end
+//     of the transform's record range: the records under it are [record + 8, skip))
 //   kind kListAcc: an accelerated list (record = LISTACC, skip = index after its tree's copies,
 //     aux = steps per copy): sets the ray's box padding; its tree follows in pre-order (one copy,
 //     or eight: copy k visits a node's children nearer-first for rays whose direction is negative
@@ -258,6 +259,9 @@ struct RenderParams {
   uint32_t frame_tiles;
   uint32_t frame_tile;
   Magic div_frame_tile, div_width;
+  // 1: no transform of the threaded program nests in another (every primitive under a transform lies
+  // in that transform's record range; the kernel may keep a hit's model-space ray from the trace)
+  uint32_t flat_xforms;
 };
 
 }  // namespace rt2

@@ -142,6 +142,7 @@ struct CompiledScene {
   std::vector<int> perlin_perm;
   int max_stack = 0;              // proven traversal-stack bound (entries)
   bool stack_ok = true;           // max_stack <= kTraversalStack: the stack traversal can run it
+  int lin_xform_depth = 0;        // deepest transform nesting in the threaded program (0: none)
   int bvh_nodes = 0, quads = 0, spheres = 0, lists = 0, xforms = 0, media = 0;
   int acc_lists = 0, acc_nodes = 0;  // exact list acceleration trees (rt2_layout.h LISTACC)
   int bvh_depth = 0;
