@@ -1738,10 +1738,14 @@ __device__ __forceinline__ void resolve_hit(const Nodes<kMode>& N, const HitRef&
       float4 m0 = N[xo + 4], m1 = N[xo + 5], m2 = N[xo + 6], m3 = N[xo + 7];
       p = mk((m0.x * p.x + m1.x * p.y) + (m2.x * p.z + m3.x), (m0.y * p.x + m1.y * p.y) + (m2.y * p.z + m3.y),
              (m0.z * p.x + m1.z * p.y) + (m2.z * p.z + m3.z));
-      float4 c0 = N[xo], c1 = N[xo + 1], c2 = N[xo + 2];
-      n = normalize(mk(c0.x * n.x + c0.y * n.y + c0.z * n.z, c1.x * n.x + c1.y * n.y + c1.z * n.z,
-                       c2.x * n.x + c2.y * n.y + c2.z * n.z));
-      x = bits(c1.w);
+      // (a medium's hit normal is never read: Isotropic::Scatter ignores it, Material.cpp:76-83)
+      const float4 c1 = N[xo + 1];
+      if (!(Has<F, kFeatMedium>() && kind == kMedium)) {
+        const float4 c0 = N[xo], c2 = N[xo + 2];
+        n = normalize(mk(c0.x * n.x + c0.y * n.y + c0.z * n.z, c1.x * n.x + c1.y * n.y + c1.z * n.z,
+                         c2.x * n.x + c2.y * n.y + c2.z * n.z));
+      }
+      x = bits(c1.w);  // the parent transform
     }
   }
 }
