@@ -15,6 +15,31 @@ namespace rt2 {
 
 namespace {
 
+// The 8 test words (sD, w[K], q[A], q[B], u[A], u[B], v[A], v[B]) of a unit-normal axis-aligned
+// quad (QUAD record r, axis code K + 4, rt2_layout.h QUADAA) when it is a rectangle in the A-B plane
+// (one edge along A, the other along B, the off-axis components exactly zero), with the edge along A
+// first: a quad whose u runs along B is recorded as its mirror (u and v swapped, w negated), whose
+// Quad::Hit interior coordinates are (beta, alpha) of the original, bit for bit (a - b = -(b - a)
+// and negation commutes with rounding), so the [0, 1]^2 test decides the same. The kernel's
+// rectangle test then reads u[A] and v[B] only. False for other quads (kept on the general path).
+bool RectAAWords(const float* r, int k, float out[8]) {
+  const int a = (k + 1) % 3, b = (k + 2) % 3;
+  const float* u = r + 8;
+  const float* v = r + 12;
+  const float wk = r[16 + k];
+  if (u[b] == 0.0f && v[a] == 0.0f) {
+    const float rec[8] = {r[19], wk, r[4 + a], r[4 + b], u[a], u[b], v[a], v[b]};
+    std::copy(rec, rec + 8, out);
+    return true;
+  }
+  if (u[a] == 0.0f && v[b] == 0.0f) {
+    const float rec[8] = {r[19], -wk, r[4 + a], r[4 + b], v[a], v[b], u[a], u[b]};
+    std::copy(rec, rec + 8, out);
+    return true;
+  }
+  return false;
+}
+
 struct Flattener {
   const Scene& s;
   CompiledScene& out;
@@ -378,9 +403,8 @@ struct Flattener {
       uint32_t axis;
       memcpy(&axis, &r[11], 4);
       if (axis < 4 || axis > 6) return 0;
-      const int kk = (int)axis - 4, a = (kk + 1) % 3, b = (kk + 2) % 3;
-      // (sD, w[K], q[A], q[B], u[A], u[B], v[A], v[B]) of QUAD (n, D | q, mat | u, axis | v | w, sD)
-      const float rec[8] = {r[19], r[16 + kk], r[4 + a], r[4 + b], r[8 + a], r[8 + b], r[12 + a], r[12 + b]};
+      float rec[8];
+      if (!RectAAWords(r, (int)axis - 4, rec)) return 0;
       words.insert(words.end(), rec, rec + 8);
       codes |= (axis - 4) << (3 * k);
     }
@@ -486,16 +510,17 @@ struct Flattener {
         uint32_t off = CopyRecords(src, kQuadRecords, lind);
         uint32_t axis;
         memcpy(&axis, &lind[4 * (off + 2) + 3], 4);
+        const float* r = out.nodes.data() + 4 * (size_t)src;
+        float test[8];
+        // a unit-normal quad that is not a rectangle in its plane takes the axis-aligned test
+        // with division (code K + 1: the same decision and t)
+        if (axis >= 4 && axis <= 6 && !RectAAWords(r, (int)axis - 4, test)) axis -= 3;
         lind_axis[off] = axis;
         if (axis >= 4 && axis <= 6) {  // QUADAA layout (rt2_layout.h)
-          const int k = (int)axis - 4, a = (k + 1) % 3, b = (k + 2) % 3;
-          const float* r = out.nodes.data() + 4 * (size_t)src;
           const float n[3] = {r[0], r[1], r[2]}, d = r[3], q[3] = {r[4], r[5], r[6]}, mat = r[7];
-          const float u[3] = {r[8], r[9], r[10]}, v[3] = {r[12], r[13], r[14]}, w[3] = {r[16], r[17], r[18]};
-          const float sd = r[19];
-          const float rec[20] = {sd,   w[k], q[a], q[b], u[a], u[b],        v[a], v[b], n[0], n[1],
-                                 n[2], d,    q[0], q[1], q[2], mat, Bits(axis), Bits(parent_xf), 0, 0};
-          std::copy(rec, rec + 20, lind.begin() + 4 * (long)off);
+          const float rec[12] = {n[0], n[1], n[2], d, q[0], q[1], q[2], mat, Bits(axis), Bits(parent_xf), 0, 0};
+          std::copy(test, test + 8, lind.begin() + 4 * (long)off);
+          std::copy(rec, rec + 12, lind.begin() + 4 * (long)off + 8);
         } else {
           lind[4 * (off + 3) + 3] = Bits(parent_xf);  // enclosing transform of this occurrence
         }

@@ -89,6 +89,9 @@ constexpr int kBlock = 256;
 #ifndef RT2_STAGE
 #define RT2_STAGE 1  // 0: samples written with plain 12-B stores (no LDS staging)
 #endif
+#ifndef RT2_QUAD_RECT
+#define RT2_QUAD_RECT 1  // QUADAA records are rectangles, edge along A first (compile.cpp RectAAWords)
+#endif
 #ifndef RT2_XRAY
 #define RT2_XRAY 1  // the Cornell kernel keeps the hit's model-space ray from the trace (resolve_hit)
 #endif
@@ -907,7 +910,11 @@ __device__ __forceinline__ bool quad_cand_unit(const float* w, f3 o, f3 d, f3 in
   return !(fabsf(dk) <= 1e-8f) && (0.0f <= alpha && alpha <= 1.0f) && (0.0f <= beta && beta <= 1.0f);
 }
 // Unit-normal axis-aligned Quad::Hit from a QUADAA record r = (sD, w[K], q[A], q[B], u[A], u[B],
-// v[A], v[B]): the same operations as quad_cand_unit on the same values.
+// v[A], v[B]): the operations of quad_cand_unit on the same values. The compiler records only
+// rectangles, edge along A first (compile.cpp RectAAWords: u[B] = v[A] = 0 exactly), so the
+// cross products' second terms are signed zeros and alpha = w_K (pv_A v_B), beta = w_K (u_A pv_B)
+// decide the same (a non-finite pv_A or pv_B, which gave a NaN, now gives a non-finite alpha or
+// beta: rejected either way).
 template <int K>
 __device__ __forceinline__ bool quad_aa(const float* r, f3 o, f3 d, f3 inv, float& t_out) {
   constexpr int A = (K + 1) % 3, B = (K + 2) % 3;
@@ -915,8 +922,13 @@ __device__ __forceinline__ bool quad_aa(const float* r, f3 o, f3 d, f3 inv, floa
   const float t = div_by_inv(r[0] - comp<K>(o), dk, comp<K>(inv));
   const float pva = (comp<A>(o) + comp<A>(d) * t) - r[2];
   const float pvb = (comp<B>(o) + comp<B>(d) * t) - r[3];
+#if RT2_QUAD_RECT
+  const float alpha = r[1] * (pva * r[7]);  // w . cross(pv, v)
+  const float beta = r[1] * (r[4] * pvb);   // w . cross(u, pv)
+#else
   const float alpha = r[1] * (pva * r[7] - r[6] * pvb);  // w . cross(pv, v)
   const float beta = r[1] * (r[4] * pvb - pva * r[5]);   // w . cross(u, pv)
+#endif
   t_out = t;
   return !(fabsf(dk) <= 1e-8f) && (0.0f <= alpha && alpha <= 1.0f) && (0.0f <= beta && beta <= 1.0f);
 }
@@ -1092,8 +1104,13 @@ __device__ __forceinline__ bool quad_aa_div(const uint32_t* r, f3 o, f3 d, float
   const float t = (uf(r[0]) - comp<K>(o)) / dk;
   const float pva = (comp<A>(o) + comp<A>(d) * t) - uf(r[2]);
   const float pvb = (comp<B>(o) + comp<B>(d) * t) - uf(r[3]);
+#if RT2_QUAD_RECT  // rectangles only, edge along A first (quad_aa)
+  const float alpha = uf(r[1]) * (pva * uf(r[7]));
+  const float beta = uf(r[1]) * (uf(r[4]) * pvb);
+#else
   const float alpha = uf(r[1]) * (pva * uf(r[7]) - uf(r[6]) * pvb);
   const float beta = uf(r[1]) * (uf(r[4]) * pvb - pva * uf(r[5]));
+#endif
   t_out = t;
   return !(fabsf(dk) <= 1e-8f) && (0.0f <= alpha && alpha <= 1.0f) && (0.0f <= beta && beta <= 1.0f);
 }

@@ -69,10 +69,12 @@ inline constexpr uint32_t make_ref(uint32_t kind, uint32_t off) { return (kind <
 //          axis = k + 1 when n and w are exactly zero off axis k (exact axis-aligned test),
 //          k + 4 when moreover n[k] = s = +-1 exactly (sD = s * D), else 0
 //          In the threaded program's record copy (lind), v.w = the enclosing XFORM's lind ref.
-//  QUADAA: (threaded-program record copy of a quad with axis code K + 4)
+//  QUADAA: (threaded-program record copy of a quad with axis code K + 4 that is a rectangle in
+//          its plane; other unit-normal quads get code K + 1 in the program)
 //          (sD, w[K], q[A], q[B]) (u[A], u[B], v[A], v[B]) (n.xyz, D) (q.xyz, material bits)
-//          (axis bits, xform ref bits, 0, 0), A = (K + 1) % 3, B = (K + 2) % 3: the test reads
-//          the first 8 words only
+//          (axis bits, xform ref bits, 0, 0), A = (K + 1) % 3, B = (K + 2) % 3, with u[B] = v[A] = 0
+//          (a quad whose u runs along B is recorded mirrored: u, v swapped and w[K] negated,
+//          compile.cpp RectAAWords): the test reads the first 8 words only
 //  SPHERE: (c0.xyz, radius) (displacement.xyz, material bits)
 //  LIST  : (count bits, flags bits, 0, 0) then child refs, 4 per record. flags bit0 = every
 //          child is a QUAD or SPHERE (iterated inline, no stack traffic).

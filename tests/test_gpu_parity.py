@@ -261,3 +261,34 @@ def test_ragged_and_tiny_images(have_gpu, w, h):
     assert st["rays"] == o_cnt["rays"] and st["paths"] == w * h * 5
     assert np.array_equal(acc.view(np.uint32), o_acc.view(np.uint32))
 
+
+
+@pytest.mark.parametrize("mode", ["linear", "stack_global"])
+def test_axis_aligned_quad_shapes(have_gpu, tmp_path, monkeypatch, mode):
+    """Axis-aligned quads in every orientation the compiler distinguishes (compile.cpp RectAAWords):
+    rectangles with u along the plane's first or second axis (the threaded program's mirrored
+    record), parallelograms (demoted to the axis-aligned test with division) and a sheared box under
+    a transform, plus a smoke box: bit-identical to the oracle."""
+    for k, v in MODES[mode].items():
+        monkeypatch.setenv(k, v)
+    from raytrace2_amd import authoring as A
+    doc = A.SceneDoc()
+    A._cornell_room(doc)
+    A._cornell_camera(doc)
+    white = doc.lambertian([0.73, 0.73, 0.73])
+    blue = doc.lambertian([0.1, 0.2, 0.7])
+    for q, u, v, m in (([100, 100, 300], [0, 0, 120], [150, 0, 0], blue),        # y plane, u along B
+                       ([300, 40, 200], [120, 0, 0], [60, 0, 140], white),       # parallelogram
+                       ([80, 200, 400], [0, 90, 30], [0, 0, 150], blue),         # x plane, sheared
+                       ([250, 300, 500], [0, 100, 0], [140, 0, 0], white)):      # z plane, u along B
+        doc.node(doc.quad(q, u, v, m))
+    doc.node(doc.quad([0, 0, 0], [90, 0, 0], [30, 0, 90], white), xform=A.transform([330, 120, 150], [25, 0, 1, 0]))
+    doc.node(doc.box([0, 0, 0], [100, 150, 100], 0, constant_medium=A.medium(0.02, [0.9, 0.9, 0.9])),
+             xform=A.transform([160, 0, 120], [-30, 0, 1, 0]))
+    p = str(tmp_path / "quads.json")
+    doc.dump(p)
+    acc, rc, st, _ = gpu_render(p, 64, 64, 16, 6)
+    o_acc, o_rc, o_cnt = oracle_render(p, 64, 64, 16, 6, forward=True)
+    assert st["overflow"] == 0
+    np.testing.assert_array_equal(rc, o_rc)
+    assert np.array_equal(acc.view(np.uint32), o_acc.view(np.uint32))
