@@ -49,7 +49,7 @@ VALU_PEAK_TLANE_OPS = SIMDS * 32 * MAX_CLOCK_HZ / 1e12  # 78.64 T lane-ops/s
 REC_BYTES = {"bvh_tests": 32, "quad_tests": 80, "sphere_tests": 32, "xform_visits": 128, "medium_tests": 16,
              "list_visits": 16}
 FLOPS = {"bvh_tests": 18, "quad_tests": 45, "sphere_tests": 30, "xform_visits": 45, "medium_tests": 20}
-KERNEL_SOURCES = ["raytrace2_amd/csrc/render.hip", "raytrace2_amd/csrc/rt2_layout.h"]
+KERNEL_SOURCES = ["raytrace2_amd/csrc/render.hip", "raytrace2_amd/csrc/rt2_layout.h", "raytrace2_amd/csrc/Makefile"]
 
 
 def kernel_sha() -> str:

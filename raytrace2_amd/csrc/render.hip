@@ -930,7 +930,8 @@ __device__ __forceinline__ bool quad_aa(const float* r, f3 o, f3 d, f3 inv, floa
   const float beta = r[1] * (r[4] * pvb - pva * r[5]);   // w . cross(u, pv)
 #endif
   t_out = t;
-  return !(fabsf(dk) <= 1e-8f) && (0.0f <= alpha && alpha <= 1.0f) && (0.0f <= beta && beta <= 1.0f);
+  // (bitwise: both coordinates are computed for every lane, no divergent branch)
+  return !(fabsf(dk) <= 1e-8f) & (0.0f <= alpha) & (alpha <= 1.0f) & (0.0f <= beta) & (beta <= 1.0f);
 }
 __device__ __forceinline__ bool quad_aa_k(uint32_t k, const float* r, f3 o, f3 d, f3 inv, float& t) {
   if (k == 0u) return quad_aa<0>(r, o, d, inv, t);
@@ -1561,7 +1562,7 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
           asm volatile("" ::"v"(t2), "v"((int)ok2));
         }
 #endif
-        if (ok0 && tmin <= t0 && t0 <= tmax) {
+        if (ok0 & (tmin <= t0) & (t0 <= tmax)) {
           tmax = t0;
           prim = make_ref(kind0, o0);
         }
