@@ -92,6 +92,12 @@ constexpr int kBlock = 256;
 #ifndef RT2_QUAD_RECT
 #define RT2_QUAD_RECT 1  // QUADAA records are rectangles, edge along A first (compile.cpp RectAAWords)
 #endif
+#ifndef RT2_UKEY
+#define RT2_UKEY 1  // quad range tests as unsigned compares of float bits (unit_pair, in_interval)
+#endif
+#ifndef RT2_BVH_SELECT
+#define RT2_BVH_SELECT 1  // lockstep BVH steps: lanes take the step's result by a select, no branch
+#endif
 #ifndef RT2_XRAY
 #define RT2_XRAY 1  // the Cornell kernel keeps the hit's model-space ray from the trace (resolve_hit)
 #endif
@@ -909,6 +915,20 @@ __device__ __forceinline__ bool quad_cand_unit(const float* w, f3 o, f3 d, f3 in
   t_out = t;
   return !(fabsf(dk) <= 1e-8f) && (0.0f <= alpha && alpha <= 1.0f) && (0.0f <= beta && beta <= 1.0f);
 }
+// Range tests as unsigned compares of the float bits (each is one comparison mask instead of two
+// and a scalar AND: the lockstep kernels are bound by the scalar unit). Exact for every input:
+// 0 <= a <= 1 and 0 <= b <= 1 (IEEE compares) <=> max(bits(a + 0), bits(b + 0)) <= bits(1.0f):
+// x + 0 maps -0 to +0 and nothing else changes; any other negative value or a NaN has an image above
+// bits(1.0f).
+__device__ __forceinline__ bool unit_pair(float a, float b) {
+  return max(__float_as_uint(a + 0.0f), __float_as_uint(b + 0.0f)) <= 0x3F800000u;
+}
+// lo <= t <= hi (IEEE compares) for 0 < lo <= hi <= FLT_MAX <=> bits(t) - bits(lo) <= bits(hi) -
+// bits(lo) (unsigned, wrapping): positive floats order as their bits; a t below lo, a negative t,
+// -0, +inf or a NaN lands above the largest right side bits(FLT_MAX) - bits(lo).
+__device__ __forceinline__ bool in_interval(float t, float lo, float hi) {
+  return __float_as_uint(t) - __float_as_uint(lo) <= __float_as_uint(hi) - __float_as_uint(lo);
+}
 // Unit-normal axis-aligned Quad::Hit from a QUADAA record r = (sD, w[K], q[A], q[B], u[A], u[B],
 // v[A], v[B]): the operations of quad_cand_unit on the same values. The compiler records only
 // rectangles, edge along A first (compile.cpp RectAAWords: u[B] = v[A] = 0 exactly), so the
@@ -931,7 +951,11 @@ __device__ __forceinline__ bool quad_aa(const float* r, f3 o, f3 d, f3 inv, floa
 #endif
   t_out = t;
   // (bitwise: both coordinates are computed for every lane, no divergent branch)
+#if RT2_UKEY
+  return !(fabsf(dk) <= 1e-8f) & unit_pair(alpha, beta);
+#else
   return !(fabsf(dk) <= 1e-8f) & (0.0f <= alpha) & (alpha <= 1.0f) & (0.0f <= beta) & (beta <= 1.0f);
+#endif
 }
 __device__ __forceinline__ bool quad_aa_k(uint32_t k, const float* r, f3 o, f3 d, f3 inv, float& t) {
   if (k == 0u) return quad_aa<0>(r, o, d, inv, t);
@@ -1113,7 +1137,11 @@ __device__ __forceinline__ bool quad_aa_div(const uint32_t* r, f3 o, f3 d, float
   const float beta = uf(r[1]) * (uf(r[4]) * pvb - pva * uf(r[5]));
 #endif
   t_out = t;
+#if RT2_UKEY
+  return !(fabsf(dk) <= 1e-8f) & unit_pair(alpha, beta);
+#else
   return !(fabsf(dk) <= 1e-8f) && (0.0f <= alpha && alpha <= 1.0f) && (0.0f <= beta && beta <= 1.0f);
+#endif
 }
 // The words come two quads (one 64-byte scalar load) at a time: no dependent loads, few SGPRs.
 __device__ __forceinline__ bool boundary_aa(const void* recs, uint32_t off, uint32_t hdr, f3 o, f3 d, float lo,
@@ -1139,7 +1167,7 @@ __device__ __forceinline__ bool boundary_aa(const void* recs, uint32_t off, uint
           ok = quad_aa_div<2>(r, o, d, t);
         }
         cnt.quad++;
-        if (ok && lo <= t && t <= hi) {
+        if (ok & (lo <= t) & (t <= hi)) {
           any = true;
           hi = t;
         }
@@ -1473,8 +1501,13 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
       do {
         RT2_WAVE(1);
         RT2_WAVE(2);
-        if (next == i) {
-          if (kStats) cnt.bvh++;
+        // kSel: every lane evaluates the step (the same VALU issue: masked lanes cost their slots
+        // anyway) and the lanes at it take the result by a select, no exec-mask branch per step
+        // (Cornell +0.4 %; the sphere kernels keep the branch: book 1 -0.4 % with the select)
+        constexpr bool kSel = RT2_BVH_SELECT && !Has<F, kFeatSphere>();
+        const bool act = next == i;
+        if (kSel || act) {
+          if (kStats && act) cnt.bvh++;
           const float4 lo = make_float4(uf(sw[4]), uf(sw[5]), uf(sw[6]), 0.0f);
           const float4 hi = make_float4(uf(sw[8]), uf(sw[9]), uf(sw[10]), 0.0f);
           const bool in = allfin ? aabb_hit_fin(lo, hi, o, inv, tmin, tmax) : aabb_hit(lo, hi, o, inv, tmin, tmax);
@@ -1484,7 +1517,7 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
             const float4 hi2 = make_float4(uf(sw[13]), uf(sw[14]), uf(sw[15]), 0.0f);
             const bool in2 =
                 allfin ? aabb_hit_fin(lo2, hi2, o, inv, tmin, tmax) : aabb_hit(lo2, hi2, o, inv, tmin, tmax);
-            if (kStats && in) cnt.bvh++;
+            if (kStats && act && in) cnt.bvh++;
             nx = in ? (in2 ? sw[2] : sw[3]) : sw[1];
           }
 #if RT2_EXP_TWICE & 8
@@ -1495,7 +1528,7 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
             asm volatile("" ::"v"((int)in2));
           }
 #endif
-          next = nx;
+          next = kSel && !act ? next : nx;
         }
         i = wave_min_next(next);
         if (i >= len) break;
@@ -1562,7 +1595,11 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
           asm volatile("" ::"v"(t2), "v"((int)ok2));
         }
 #endif
+#if RT2_UKEY
+        if (ok0 & in_interval(t0, tmin, tmax)) {
+#else
         if (ok0 & (tmin <= t0) & (t0 <= tmax)) {
+#endif
           tmax = t0;
           prim = make_ref(kind0, o0);
         }
