@@ -952,7 +952,7 @@ __device__ __forceinline__ bool quad_aa(const float* r, f3 o, f3 d, f3 inv, floa
   t_out = t;
   // (bitwise: both coordinates are computed for every lane, no divergent branch)
 #if RT2_UKEY
-  return !(fabsf(dk) <= 1e-8f) & unit_pair(alpha, beta);
+  return (int)!(fabsf(dk) <= 1e-8f) & (int)unit_pair(alpha, beta);
 #else
   return !(fabsf(dk) <= 1e-8f) & (0.0f <= alpha) & (alpha <= 1.0f) & (0.0f <= beta) & (beta <= 1.0f);
 #endif
@@ -1138,7 +1138,7 @@ __device__ __forceinline__ bool quad_aa_div(const uint32_t* r, f3 o, f3 d, float
 #endif
   t_out = t;
 #if RT2_UKEY
-  return !(fabsf(dk) <= 1e-8f) & unit_pair(alpha, beta);
+  return (int)!(fabsf(dk) <= 1e-8f) & (int)unit_pair(alpha, beta);
 #else
   return !(fabsf(dk) <= 1e-8f) && (0.0f <= alpha && alpha <= 1.0f) && (0.0f <= beta && beta <= 1.0f);
 #endif
