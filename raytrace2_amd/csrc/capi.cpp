@@ -972,6 +972,10 @@ int LaunchFrames(rt2_tracer* t, int n_frames) {
   p.max_depth = t->max_depth;
   p.seed_lo = (uint32_t)t->seed;
   p.seed_hi = (uint32_t)(t->seed >> 32);
+  for (uint32_t r = 0; r < 10; r++) {
+    p.philox_keys[2 * r] = p.seed_lo + r * 0x9E3779B9u;
+    p.philox_keys[2 * r + 1] = p.seed_hi + r * 0xBB67AE85u;
+  }
   p.ray_counts = t->d_ray_counts;
   p.work_counter = t->d_work;
   p.stats = t->d_stats;

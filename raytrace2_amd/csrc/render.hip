@@ -98,6 +98,9 @@ constexpr int kBlock = 256;
 #ifndef RT2_BVH_SELECT
 #define RT2_BVH_SELECT 1  // lockstep BVH steps: lanes take the step's result by a select, no branch
 #endif
+#ifndef RT2_PHILOX_RK
+#define RT2_PHILOX_RK 1  // path-stream Philox round keys precomputed on the host (philox_path)
+#endif
 #ifndef RT2_XRAY
 #define RT2_XRAY 1  // the Cornell kernel keeps the hit's model-space ray from the trace (resolve_hit)
 #endif
@@ -417,6 +420,42 @@ __device__ __forceinline__ void philox(uint32_t k0, uint32_t k1, uint32_t pixel,
   r3 = c3;
 }
 
+// philox() with the path streams' round keys from the launch parameters (RenderParams::philox_keys,
+// two scalar loads): the same rounds and values, no scalar adds (kRK; Cornell +0.5 %, volume +0.7 %;
+// the sphere kernels keep the adds: the 20 key SGPRs cost book 1 SGPR spills, -0.4 %).
+template <bool kRK>
+__device__ __forceinline__ void philox_path(uint32_t pixel, uint32_t frame, uint32_t block, uint32_t& r0,
+                                            uint32_t& r1, uint32_t& r2, uint32_t& r3) {
+  if constexpr (!(RT2_PHILOX_RK && kRK)) {
+    uint32_t key0, key1;
+    seed_args(key0, key1);
+    philox(key0, key1, pixel, frame, block, r0, r1, r2, r3);
+    return;
+  }
+  static_assert(RT2_KOFF(philox_keys) % 4 == 0, "RenderParams layout");
+  const u32x16 ka = karg16<RT2_KOFF(philox_keys)>();
+  const u32x4 kb = karg4<RT2_KOFF(philox_keys) + 64u>();
+  uint32_t c0 = pixel, c1 = frame, c2 = block, c3 = 0x52543250u;
+  const uint32_t m0 = 0xD2511F53u, m1 = 0xCD9E8D57u;
+#pragma unroll
+  for (int r = 0; r < 10; r++) {
+    const uint32_t key0 = r < 8 ? ka[2 * r] : kb[2 * r - 16], key1 = r < 8 ? ka[2 * r + 1] : kb[2 * r - 15];
+    uint64_t p0, p1;
+    asm("v_mad_u64_u32 %0, vcc, %1, %2, 0" : "=v"(p0) : "s"(m0), "v"(c0) : "vcc");
+    asm("v_mad_u64_u32 %0, vcc, %1, %2, 0" : "=v"(p1) : "s"(m1), "v"(c2) : "vcc");
+    const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(c0) : "v"(hi1), "v"(c1), "s"(key0));
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(c2) : "v"(hi0), "v"(c3), "s"(key1));
+    c1 = lo1;
+    c3 = lo0;
+  }
+  r0 = c0;
+  r1 = c1;
+  r2 = c2;
+  r3 = c3;
+}
+
 __device__ __forceinline__ uint32_t sel4(uint32_t i, uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3) {
   return i == 0u ? r0 : (i == 1u ? r1 : (i == 2u ? r2 : r3));
 }
@@ -439,7 +478,7 @@ typedef __attribute__((address_space(3))) float lds_f32;
 // code at every draw site where any lane refills: the scatter site and the camera site of the
 // lanes that start a path, both in nearly every bounce (profiles/r04_c2_cost_probes.json). The
 // draws are the same values in the same order.
-template <bool kLdsRng, bool kRing = false>
+template <bool kLdsRng, bool kRing = false, bool kRK = false>
 struct PathT {
   static constexpr bool kLds = kLdsRng;
   uint32_t frame;
@@ -458,17 +497,16 @@ struct PathT {
     n = 4u << 28;
   }
   __device__ __forceinline__ void block(uint32_t b, uint32_t& w0, uint32_t& w1, uint32_t& w2, uint32_t& w3) const {
-    uint32_t key0, key1;
-    seed_args(key0, key1);  // re-read at the refill (see karg16)
-    philox(key0, key1, pix, frame, b, w0, w1, w2, w3);
+    philox_path<kRK>(pix, frame, b, w0, w1, w2, w3);  // keys re-read at the refill (see karg16)
   }
   // kRing: block b of frame f into the ring (half b & 1)
   __device__ __forceinline__ void ring_put(uint32_t f, uint32_t b) {
-    uint32_t key0, key1, w0, w1, w2, w3;
-    seed_args(key0, key1);
-    philox(key0, key1, pix, f, b, w0, w1, w2, w3);
+    uint32_t w0, w1, w2, w3;
+    philox_path<kRK>(pix, f, b, w0, w1, w2, w3);
 #if RT2_EXP_TWICE & 256
     {
+      uint32_t key0, key1;
+      seed_args(key0, key1);
       uint32_t q0, q1, q2, q3, fr = f;
       asm volatile("" : "+v"(fr));
       philox(key0, key1, pix, fr, b + 7u, q0, q1, q2, q3);
@@ -2036,7 +2074,7 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
   uint32_t bnext = 0, bend = 0;  // the wave's reserved batch of work items (wave-uniform)
   uint32_t item_rays = 0;
   constexpr bool kRing = Ring<F, kMode, kStats>();  // two-block Philox ring
-  PathT<kLdsRng, kRing> path;
+  PathT<kLdsRng, kRing, !Has<F, kFeatSphere>()> path;
   path.rb = lp + 64u * kRngP;
   lds_u32* pk = lp + 64u * kParkP;  // this lane's park planes (kPark)
   path.pix = 0;

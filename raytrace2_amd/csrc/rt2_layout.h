@@ -264,6 +264,10 @@ struct RenderParams {
   // 1: no transform of the threaded program nests in another (every primitive under a transform lies
   // in that transform's record range; the kernel may keep a hit's model-space ray from the trace)
   uint32_t flat_xforms;
+  // Philox4x32-10 round keys of the path streams: (seed_lo + r * 0x9E3779B9, seed_hi + r * 0xBB67AE85)
+  // for rounds r = 0..9, interleaved (the kernel loads them with two scalar loads per block instead
+  // of computing 18 adds on the scalar unit at every refill)
+  uint32_t philox_keys[20];
 };
 
 }  // namespace rt2
