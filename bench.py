@@ -20,7 +20,7 @@ Multi-GPU goes through the C ABI (include/rt2.h), not torch:
     split (all: every rank in turn); no gather.
 
 Rank 0 prints one JSON line (contract in the task statement) with a `roofline` object for the render
-kernel (bound: VALU issue; PMC instruction density from a committed profile of this kernel build and
+kernel (bound: VALU or scalar issue; PMC instruction density from a committed profile of this kernel build and
 config x the live rays / HIP-event launch time) and a `cpu_baseline` object (the oracle restatement
 on every host core this process may use, bounded sample).
 """
@@ -45,6 +45,8 @@ MAX_CLOCK_HZ = 2.4e9           # MI355X_MICROARCH.md "Max clock"
 SIMDS = 256 * 4
 # VALU issue peak: a wave64 VALU instruction occupies a 32-lane SIMD for 2 cycles
 VALU_PEAK_TLANE_OPS = SIMDS * 32 * MAX_CLOCK_HZ / 1e12  # 78.64 T lane-ops/s
+# Scalar issue peak: one scalar unit per CU (MI355X_MICROARCH.md), one SALU instruction per cycle
+SALU_PEAK_GINST = 256 * MAX_CLOCK_HZ / 1e9  # 614.4 G instructions/s
 # Record sizes of the flattened scene program (rt2_layout.h) in bytes
 REC_BYTES = {"bvh_tests": 32, "quad_tests": 80, "sphere_tests": 32, "xform_visits": 128, "medium_tests": 16,
              "list_visits": 16}
@@ -146,9 +148,11 @@ def find_profile(key):
 
 
 def roofline_for(tr, rays_local, launches, kernel_ms, key, rank_stats_frames, spp_total):
-    """Roofline of the render kernel on this GPU: bound = VALU issue (the kernel is issue bound,
-    DESIGN.md §4 Roofline). `achieved` = VALU lane-operations per second = the VALU instructions per
-    ray of the matching PMC profile x this run's rays per launch / this run's HIP-event launch time.
+    """Roofline of the render kernel on this GPU: the kernel is issue bound (DESIGN.md §4 Roofline),
+    on the vector pipe (VALU lane-operations per second = the VALU instructions per ray of the
+    matching PMC profile x 64 x this run's rays per launch / this run's HIP-event launch time) or on
+    the CU's one scalar unit (SALU instructions per second, same scaling); `bound` is the pipe with
+    the larger fraction of its peak, and both fractions are reported (valu_frac, salu_frac).
     Also: the HBM fraction (profile traffic per ray, same scaling), the §8(d) useful-flop fraction
     and the scene-record rate (bytes of records touched per ray / launch time, not an HBM figure)."""
     tr.enable_stats(True)
@@ -170,8 +174,16 @@ def roofline_for(tr, rays_local, launches, kernel_ms, key, rank_stats_frames, sp
     if prof:
         pr = prof["per_ray"]
         valu = pr["valu_insts"] * rays_per_launch  # wave instructions per launch
-        out["achieved"] = round(valu * 64 / avg_launch_s / 1e12, 3)
-        out["frac"] = round(out["achieved"] / VALU_PEAK_TLANE_OPS, 4)
+        salu = pr.get("salu_insts", 0.0) * rays_per_launch
+        valu_rate = valu * 64 / avg_launch_s / 1e12
+        salu_rate = salu / avg_launch_s / 1e9
+        out["valu_frac"] = round(valu_rate / VALU_PEAK_TLANE_OPS, 4)
+        out["salu_frac"] = round(salu_rate / SALU_PEAK_GINST, 4)
+        if out["salu_frac"] > out["valu_frac"]:
+            out.update(bound="salu_issue", unit="Ginst/s", peak=round(SALU_PEAK_GINST, 1),
+                       achieved=round(salu_rate, 2), frac=out["salu_frac"])
+        else:
+            out.update(achieved=round(valu_rate, 3), frac=out["valu_frac"])
         out["valu_insts_per_ray"] = round(pr["valu_insts"], 3)
         out["salu_insts_per_ray"] = round(pr.get("salu_insts", 0.0), 3)
         if pr.get("hbm_bytes") is not None:
