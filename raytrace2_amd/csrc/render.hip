@@ -2377,6 +2377,9 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
       for (int rep2 = 0; rep2 < 2; rep2++) {
         asm volatile("" : "+v"(color.x), "+v"(color.y), "+v"(color.z));
 #endif
+#if RT2_EXP_NOSTORE  // diagnostic (tools/c5_traffic.sh): no sample store, to attribute HBM writes
+      if (false)
+#endif
       if constexpr (kGroup != 0u) {
         lds_f32* oct = (lds_f32*)(lp + 64u * kOctP);
         const uint32_t gs = slot & (kGroup - 1u);  // slot within the group = LDS slot

@@ -1,10 +1,11 @@
 #!/bin/bash
 # Book 2 (C5) HBM traffic attribution: FETCH_SIZE / WRITE_SIZE passes of one render step (spp 1000)
-# with the accelerated list's tree in one copy (RT2_ACC_OCTANTS=0) and in eight octant copies.
+# with the accelerated list's tree in one copy (RT2_ACC_OCTANTS=0) and in eight octant copies; RT2_LIB
+# (absolute path) selects a build, e.g. the RT2_EXP_NOSTORE=1 diagnostic; TAG names the output dir.
 set -u
 cd /tmp && export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-/root/repo}
-OUT=$R/gpurun_out/c5traffic
+OUT=$R/gpurun_out/${TAG:-c5traffic}
 rm -rf $OUT; mkdir -p $OUT
 B2="--scene book2_final_scene_10000_samples.json --width 800 --height 800 --spp ${SPP:-1000}"
 for oct in ${OCTS:-1 0}; do
