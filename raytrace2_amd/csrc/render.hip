@@ -1590,32 +1590,31 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
       // order (issue-bound: one candidate at a time beats two interleaved, measured)
       const uint32_t run = st.w;
       uint32_t codes = st.y;
-      // ref = the quad's QUADAA ref (kind bits | record offset): ref << 4 is the record's byte
-      // offset (the kind bits shift out of 32 bits) and the loop runs to the run's end ref, so one
-      // scalar add per quad keeps the offset, the hit ref and the loop bound
-      const uint32_t ref0 = make_ref(kQuadAA, off), ref_end = ref0 + 5u * run;
-      for (uint32_t ref = ref0; ref != ref_end; ref += 5u, codes >>= 3) {
+      for (uint32_t k = 0; k < run; k++, codes >>= 3) {
+        const uint32_t o0 = off + 5u * k;
         const uint32_t c0 = codes & 7u;
         float t0;
         bool ok0;
-        uint32_t ref_hit = ref;
+        uint32_t kind0;
         if (c0 >= 4u) {
-          const u32x8 a = sld8(recs, ref << 4);  // (the first quad's words are also inline in sw)
+          const u32x8 a = k == 0u ? u32x8{sw[4], sw[5], sw[6], sw[7], sw[8], sw[9], sw[10], sw[11]}
+                                  : sld8(recs, o0 * 16u);
           float ra[8];
 #pragma unroll
           for (int j = 0; j < 8; j++) ra[j] = uf(a[j]);
           ok0 = quad_aa_k(c0 - 4u, ra, o, d, inv, t0);
+          kind0 = kQuadAA;
         } else {
           u32x16 a;
           u32x4 b2;
-          sld20(recs, ref << 4, a, b2);
+          sld20(recs, o0 * 16u, a, b2);
           float w0[20];
 #pragma unroll
           for (int j = 0; j < 16; j++) w0[j] = uf(a[j]);
 #pragma unroll
           for (int j = 0; j < 4; j++) w0[16 + j] = uf(b2[j]);
           ok0 = quad_cand_u(c0, w0, o, d, inv, t0);
-          ref_hit = ref ^ ((kQuadAA ^ kQuad) << 28);  // QUAD layout
+          kind0 = kQuad;
         }
         if (kStats) cnt.quad += 1;
 #if RT2_EXP_TWICE & 16
@@ -1625,7 +1624,7 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
           float t2 = 0.0f;
           bool ok2 = false;
           if (c0 >= 4u) {
-            const u32x8 a = sld8(recs, ref << 4);
+            const u32x8 a = sld8(recs, o0 * 16u);
             float ra[8];
 #pragma unroll
             for (int j = 0; j < 8; j++) ra[j] = uf(a[j]);
@@ -1640,7 +1639,7 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
         if (ok0 & (tmin <= t0) & (t0 <= tmax)) {
 #endif
           tmax = t0;
-          prim = ref_hit;
+          prim = make_ref(kind0, o0);
         }
       }
       next = at + run;
