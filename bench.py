@@ -361,6 +361,21 @@ def main():
                 ps = tr.part_stats(g)
                 per_rank[-1]["gpus"].append({"gpu": g, "rays": ps["rays"], "kernel_ms": ps["kernel_ms"],
                                              "enqueue_ms": ps["enqueue_ms"], "launches": ps["launches"]})
+    # One gather + readback after the timed steps with the GPU otherwise idle: the event pair around
+    # a step's gather in a run of back-to-back steps also spans the time its small kernels (the
+    # RCCL gather, the de-interleave) wait for CUs behind the next step's render, whose persistent
+    # waves hold them (gather_ms_per_step); this is the cost of the exchange itself.
+    gather_iso_ms = None
+    if mode in ("ranks", "multi") and host_gather is None:
+        sync_all()
+        if mode == "ranks":
+            dist.barrier()
+        t_g = time.perf_counter()
+        tr.gather()
+        if readback is not None:
+            tr.image_non_converted_pixels_async(readback.array.ctypes.data)
+        sync_all()
+        gather_iso_ms = round((time.perf_counter() - t_g) * 1e3, 3)
     launch_shape = tr.last_launch()  # the timed launches' shape (before the stats pass below)
     me = per_rank[-1] if mode != "emulate" else max(per_rank, key=lambda r: r["elapsed_s"])
     if mode == "ranks":
@@ -445,6 +460,7 @@ def main():
                        "kernel_sha": key["kernel_sha"], "source_kernel_sha": src_sha,
                        "kernel_ms_per_step_max": round(max(r["kernel_ms"] for r in per_rank) / a.steps, 2),
                        "gather_ms_per_step": round(per_rank[0]["gather_ms"] / a.steps, 3),
+                       "gather_readback_ms_isolated": gather_iso_ms,
                        "readback_ms_per_step": round(per_rank[0]["readback_ms"] / a.steps, 3),
                        "readback_bytes_per_step": (a.width * a.height * 12 if per_rank[0]["readbacks"] else 0),
                        "enqueue_ms_per_step": round(per_rank[0]["enqueue_ms"] / a.steps, 3),
