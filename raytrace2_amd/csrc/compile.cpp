@@ -40,6 +40,38 @@ bool RectAAWords(const float* r, int k, float out[8]) {
   return false;
 }
 
+// The world-space normal of a quad under transforms, n_world = normalize(invM^T n) through the chain
+// of enclosing transforms innermost first (Transform.cpp:85-86), with the float operations of
+// render.hip resolve_hit in its order: each row product ((c.x n.x + c.y n.y) + c.z n.z) over the
+// XFORM record's invM columns c0..c2 (threaded-program copies, parent link in c1.w), then glm's
+// normalize v * (1 / sqrt(dot(v, v))). Every hit on the quad transforms the same normal, so the
+// kernel reads it from the record (QUADAA words 12-14) instead of computing it per hit; the sign
+// follows front_face (normalize(-v) = -normalize(v) and M(-n) = -(M n) exactly). The host build
+// rounds every operation as the device does (-ffp-contract=off, SSE single precision, correctly
+// rounded sqrt and division).
+void WorldNormal(const std::vector<float>& lind, uint32_t xf, const float n_model[3], float out[3]) {
+  float n[3] = {n_model[0], n_model[1], n_model[2]};
+  for (uint32_t x = xf; x != kRefNone;) {
+    const size_t xo = 4 * (size_t)(x & kOffsetMask);
+    const float* c0 = &lind[xo];
+    const float* c1 = &lind[xo + 4];
+    const float* c2 = &lind[xo + 8];
+    const float v[3] = {c0[0] * n[0] + c0[1] * n[1] + c0[2] * n[2], c1[0] * n[0] + c1[1] * n[1] + c1[2] * n[2],
+                        c2[0] * n[0] + c2[1] * n[1] + c2[2] * n[2]};
+    const float l2 = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
+    const float s = 1.0f / std::sqrt(l2);
+    n[0] = v[0] * s;
+    n[1] = v[1] * s;
+    n[2] = v[2] * s;
+    uint32_t parent;
+    memcpy(&parent, &c1[3], 4);
+    x = parent;
+  }
+  out[0] = n[0];
+  out[1] = n[1];
+  out[2] = n[2];
+}
+
 struct Flattener {
   const Scene& s;
   CompiledScene& out;
@@ -518,7 +550,9 @@ struct Flattener {
         lind_axis[off] = axis;
         if (axis >= 4 && axis <= 6) {  // QUADAA layout (rt2_layout.h)
           const float n[3] = {r[0], r[1], r[2]}, d = r[3], q[3] = {r[4], r[5], r[6]}, mat = r[7];
-          const float rec[12] = {n[0], n[1], n[2], d, q[0], q[1], q[2], mat, Bits(axis), Bits(parent_xf), 0, 0};
+          float w[3] = {q[0], q[1], q[2]};
+          if (parent_xf != kRefNone) WorldNormal(lind, parent_xf, n, w);  // replaces q (unused here)
+          const float rec[12] = {n[0], n[1], n[2], d, w[0], w[1], w[2], mat, Bits(axis), Bits(parent_xf), 0, 0};
           std::copy(test, test + 8, lind.begin() + 4 * (long)off);
           std::copy(rec, rec + 12, lind.begin() + 4 * (long)off + 8);
         } else {

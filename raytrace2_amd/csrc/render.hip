@@ -101,6 +101,9 @@ constexpr int kBlock = 256;
 #ifndef RT2_PHILOX_RK
 #define RT2_PHILOX_RK 1  // path-stream Philox round keys precomputed on the host (philox_path)
 #endif
+#ifndef RT2_WORLD_NORMAL
+#define RT2_WORLD_NORMAL 1  // transformed QUADAA quads carry their world normal (compile.cpp WorldNormal)
+#endif
 #ifndef RT2_XRAY
 #define RT2_XRAY 1  // the Cornell kernel keeps the hit's model-space ray from the trace (resolve_hit)
 #endif
@@ -1801,6 +1804,7 @@ __device__ __forceinline__ void resolve_hit(const Nodes<kMode>& N, const HitRef&
     }
   }
   uint32_t kind = h.prim >> 28, off = h.prim & kOffsetMask;
+  bool wnormal = false;  // n is already the world normal (QUADAA under transforms)
   p = o + d * h.t;
   if (Has<F, kFeatMedium>() && kind == kMedium) {
     n = mk(1.0f, 0.0f, 0.0f);
@@ -1817,7 +1821,19 @@ __device__ __forceinline__ void resolve_hit(const Nodes<kMode>& N, const HitRef&
     f3 qn = xyz(N[off + 2]);
     front = dot(d, qn) < 0.0f;
     n = front ? qn : -qn;
+#if RT2_WORLD_NORMAL
+    const float4 r3 = N[off + 3];
+    mat = bits(r3.w);
+    if (Has<F, kFeatXform>() && h.xf != kRefNone) {
+      // the quad's world normal from the record (compile.cpp WorldNormal: the same operations as the
+      // loop below on the same values); the loop then moves only the point
+      const f3 wn = xyz(r3);
+      n = front ? wn : -wn;
+      wnormal = true;
+    }
+#else
     mat = N.word(off + 3, 3);
+#endif
   } else {
     f3 qn = xyz(N[off]);
     front = dot(d, qn) < 0.0f;
@@ -1833,7 +1849,7 @@ __device__ __forceinline__ void resolve_hit(const Nodes<kMode>& N, const HitRef&
              (m0.z * p.x + m1.z * p.y) + (m2.z * p.z + m3.z));
       // (a medium's hit normal is never read: Isotropic::Scatter ignores it, Material.cpp:76-83)
       const float4 c1 = N[xo + 1];
-      if (!(Has<F, kFeatMedium>() && kind == kMedium)) {
+      if (!(Has<F, kFeatMedium>() && kind == kMedium) && !wnormal) {
         const float4 c0 = N[xo], c2 = N[xo + 2];
         n = normalize(mk(c0.x * n.x + c0.y * n.y + c0.z * n.z, c1.x * n.x + c1.y * n.y + c1.z * n.z,
                          c2.x * n.x + c2.y * n.y + c2.z * n.z));
