@@ -89,12 +89,6 @@ constexpr int kBlock = 256;
 #ifndef RT2_STAGE
 #define RT2_STAGE 1  // 0: samples written with plain 12-B stores (no LDS staging)
 #endif
-#ifndef RT2_QUAD_RECT
-#define RT2_QUAD_RECT 1  // QUADAA records are rectangles, edge along A first (compile.cpp RectAAWords)
-#endif
-#ifndef RT2_UKEY
-#define RT2_UKEY 1  // quad range tests as unsigned compares of float bits (unit_pair, in_interval)
-#endif
 #ifndef RT2_BVH_SELECT
 #define RT2_BVH_SELECT 1  // lockstep BVH steps: lanes take the step's result by a select, no branch
 #endif
@@ -983,20 +977,11 @@ __device__ __forceinline__ bool quad_aa(const float* r, f3 o, f3 d, f3 inv, floa
   const float t = div_by_inv(r[0] - comp<K>(o), dk, comp<K>(inv));
   const float pva = (comp<A>(o) + comp<A>(d) * t) - r[2];
   const float pvb = (comp<B>(o) + comp<B>(d) * t) - r[3];
-#if RT2_QUAD_RECT
   const float alpha = r[1] * (pva * r[7]);  // w . cross(pv, v)
   const float beta = r[1] * (r[4] * pvb);   // w . cross(u, pv)
-#else
-  const float alpha = r[1] * (pva * r[7] - r[6] * pvb);  // w . cross(pv, v)
-  const float beta = r[1] * (r[4] * pvb - pva * r[5]);   // w . cross(u, pv)
-#endif
   t_out = t;
   // (bitwise: both coordinates are computed for every lane, no divergent branch)
-#if RT2_UKEY
   return (int)!(fabsf(dk) <= 1e-8f) & (int)unit_pair(alpha, beta);
-#else
-  return !(fabsf(dk) <= 1e-8f) & (0.0f <= alpha) & (alpha <= 1.0f) & (0.0f <= beta) & (beta <= 1.0f);
-#endif
 }
 __device__ __forceinline__ bool quad_aa_k(uint32_t k, const float* r, f3 o, f3 d, f3 inv, float& t) {
   if (k == 0u) return quad_aa<0>(r, o, d, inv, t);
@@ -1170,19 +1155,10 @@ __device__ __forceinline__ bool quad_aa_div(const uint32_t* r, f3 o, f3 d, float
   const float t = (uf(r[0]) - comp<K>(o)) / dk;
   const float pva = (comp<A>(o) + comp<A>(d) * t) - uf(r[2]);
   const float pvb = (comp<B>(o) + comp<B>(d) * t) - uf(r[3]);
-#if RT2_QUAD_RECT  // rectangles only, edge along A first (quad_aa)
   const float alpha = uf(r[1]) * (pva * uf(r[7]));
   const float beta = uf(r[1]) * (uf(r[4]) * pvb);
-#else
-  const float alpha = uf(r[1]) * (pva * uf(r[7]) - uf(r[6]) * pvb);
-  const float beta = uf(r[1]) * (uf(r[4]) * pvb - pva * uf(r[5]));
-#endif
   t_out = t;
-#if RT2_UKEY
   return (int)!(fabsf(dk) <= 1e-8f) & (int)unit_pair(alpha, beta);
-#else
-  return !(fabsf(dk) <= 1e-8f) && (0.0f <= alpha && alpha <= 1.0f) && (0.0f <= beta && beta <= 1.0f);
-#endif
 }
 // The words come two quads (one 64-byte scalar load) at a time: no dependent loads, few SGPRs.
 __device__ __forceinline__ bool boundary_aa(const void* recs, uint32_t off, uint32_t hdr, f3 o, f3 d, float lo,
@@ -1636,11 +1612,7 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
           asm volatile("" ::"v"(t2), "v"((int)ok2));
         }
 #endif
-#if RT2_UKEY
         if (ok0 & in_interval(t0, tmin, tmax)) {
-#else
-        if (ok0 & (tmin <= t0) & (t0 <= tmax)) {
-#endif
           tmax = t0;
           prim = make_ref(kind0, o0);
         }
