@@ -52,7 +52,7 @@ constexpr int kBlock = 256;
 #define RT2_EXP_TWICE 0  // cost probes (bits): 1 resolve_hit, 2 rand_unit_vec3, 4 camera_ray, 8 slab test,
                          // 16 quad-run test, 32 threaded medium step, 64 its log, 128 its two boundary
                          // queries, 256 a Philox block (at every refill), 512 the sample store /
-                         // staging, 1024 the work-item decode run twice
+                         // staging, 2048 a threaded transform entry (ray into model space, its reciprocal)
 #endif
 #ifndef RT2_EXP_WAVESTEPS
 #define RT2_EXP_WAVESTEPS 0  // diagnostic build: per-wave linear-traversal step counts into diag slots
@@ -1642,6 +1642,20 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
       d = normalize(nd);
       inv = recip3(d);
       fin = finite3(inv);
+#if RT2_EXP_TWICE & 2048
+      {
+        f3 o2 = o;
+        asm volatile("" : "+v"(o2.x), "+v"(o2.y), "+v"(o2.z));
+        const f3 n2 = mk((uf(m[0]) * o2.x + uf(m[4]) * o2.y) + (uf(m[8]) * o2.z + uf(m[12])),
+                         (uf(m[1]) * o2.x + uf(m[5]) * o2.y) + (uf(m[9]) * o2.z + uf(m[13])),
+                         (uf(m[2]) * o2.x + uf(m[6]) * o2.y) + (uf(m[10]) * o2.z + uf(m[14])));
+        const f3 d2 = normalize(mk(uf(m[0]) * o2.x + uf(m[4]) * o2.y + uf(m[8]) * o2.z,
+                                   uf(m[1]) * o2.x + uf(m[5]) * o2.y + uf(m[9]) * o2.z,
+                                   uf(m[2]) * o2.x + uf(m[6]) * o2.y + uf(m[10]) * o2.z));
+        const f3 i2 = recip3(d2);
+        asm volatile("" ::"v"(n2.x), "v"(n2.y), "v"(n2.z), "v"(i2.x), "v"(i2.y), "v"(i2.z));
+      }
+#endif
       cur_xf = make_ref(kXform, off);
     } else if (Has<F, kFeatXform>() && kind == kXformExit) {
       // kept model-space ray (xray planes, flat transforms): the closest primitive so far lies under
