@@ -12,14 +12,18 @@
 * acc_slab: the accelerated-list tree's padded slab test (one fma per bound, +-2^100 for an infinite
   1/d) never culls a box that the exact padded slab test accepts, for rays with direction components
   of +-0 and origins inside the padding band (the fma form with 1/d = inf culled those).
+* rcp_nr exhaustively: every float bit pattern in its range (3.7e9 values, both signs) gives IEEE 1/x
+  with the hardware reciprocal and two Newton steps.
 """
 import pytest
 
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("which,n", [(0, 1 << 28), (1, 1 << 26), (2, 1 << 28), (3, 1 << 28), (4, 1 << 26)],
-                         ids=["div_by_inv", "aabb_fin", "rcp_sqrt_nr", "div_by_inv_any_t", "acc_slab_conservative"])
+@pytest.mark.parametrize("which,n", [(0, 1 << 28), (1, 1 << 26), (2, 1 << 28), (3, 1 << 28), (4, 1 << 26),
+                                     (5, 1 << 32)],
+                         ids=["div_by_inv", "aabb_fin", "rcp_sqrt_nr", "div_by_inv_any_t", "acc_slab_conservative",
+                              "rcp_nr_every_float"])
 def test_selftest(have_gpu, which, n):
     from raytrace2_amd._native import selftest
     bad, checked = selftest(which, n, seed=20241015)
