@@ -257,7 +257,8 @@ RT2_API int rt2_tracer_reset_stats(rt2_tracer* tr);
  * scaling; which 3: division by a correctly rounded reciprocal over any quotient, numerators down to
  * 2^-100; which 4: the accelerated-list padded slab test culls no box the exact padded slab accepts,
  * zero direction components included; which 5: the reciprocal without range scaling for every float
- * bit pattern below n, n = 2^32 for all of them). Writes the number of mismatches and of inputs checked. */
+ * bit pattern below n, n = 2^32 for all of them; which 6: division by a correctly rounded reciprocal
+ * for the first n pairs of significands, n = 2^46 for all of them). Writes the number of mismatches and of inputs checked. */
 RT2_API int rt2_selftest(int device, int which, uint64_t n, uint64_t seed, uint64_t* mismatches, uint64_t* checked);
 
 /* ---- util::WriteImage (Util.cpp:39-79): sqrt gamma, clamp(x*255.999), vertical flip ---- */

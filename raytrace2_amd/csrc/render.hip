@@ -826,16 +826,14 @@ __device__ __forceinline__ bool finite3(f3 v) {
   return __builtin_isfinite(v.x) && __builtin_isfinite(v.y) && __builtin_isfinite(v.z);
 }
 
-// a / b, correctly rounded, from inv = fl(1 / b) (correctly rounded): q0 = a * inv is within
-// 2 ulp, one fma correction makes it faithful and a second one (Markstein) correctly rounded.
-// Equal to IEEE a / b whenever no intermediate under/overflows; the callers reject every case
-// where one could (|b| <= 1e-8 or a quotient below tmin). rt2_selftest checks it on the GPU.
+// a / b, correctly rounded, from inv = fl(1 / b) (correctly rounded): q0 = a * inv and one fma
+// correction q0 + (a - b q0) inv. Equal to IEEE a / b for every pair of significands
+// (rt2_selftest which 6 checks all 2^46 pairs; the algorithm and the quotient scale exactly with the
+// exponents) whenever no intermediate under/overflows; the callers reject every case where one
+// could (|b| <= 1e-8 or a quotient below tmin), and selftests 0 and 3 check their ranges.
 __device__ __forceinline__ float div_by_inv(float a, float b, float inv) {
-  float q = a * inv;
-  float r = fmaf(-b, q, a);
-  q = fmaf(r, inv, q);
-  r = fmaf(-b, q, a);
-  return fmaf(r, inv, q);
+  const float q = a * inv;
+  return fmaf(fmaf(-b, q, a), inv, q);
 }
 
 // Quad::Hit (Quad.cpp:19-43): inclusive interval (Contains)
@@ -2595,6 +2593,7 @@ KernelFn Kernel(int v, int mode, bool stats) {
 //   which 2: rcp_nr == 1/x and sqrt_nr == sqrt(x) in their ranges
 //   which 4: acc_slab (accelerated-list padded slab) never culls a box the exact padded slab accepts
 //   which 5: rcp_nr == 1/x for every float in its range (exhaustive over the 2^32 bit patterns)
+//   which 6: div_by_inv's single correction == a / b for every pair of significands (n = 2^46)
 __device__ __forceinline__ float rand_float(uint32_t bits, int emin, int emax, uint32_t sel) {
   const int e = emin + (int)(sel % (uint32_t)(emax - emin + 1));
   return __uint_as_float((bits & 0x807FFFFFu) | ((uint32_t)(e + 127) << 23));
@@ -2603,6 +2602,15 @@ __global__ void selftest_kernel(int which, unsigned long long n, uint32_t seed, 
   unsigned long long bad = 0, checked = 0;
   for (unsigned long long idx = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; idx < n;
        idx += (unsigned long long)gridDim.x * blockDim.x) {
+    if (which == 6) {
+      // every pair of significands (n = 2^46): a, b in [1, 2); div_by_inv against IEEE a / b (the
+      // algorithm and the quotient scale exactly with the exponents)
+      const float a = __uint_as_float(0x3F800000u | (uint32_t)(idx >> 23));
+      const float b = __uint_as_float(0x3F800000u | ((uint32_t)idx & 0x7FFFFFu));
+      checked++;
+      if (__float_as_uint(div_by_inv(a, b, rcp_nr(b))) != __float_as_uint(a / b)) bad++;
+      continue;
+    }
     uint32_t r0, r1, r2, r3;
     philox(seed, 0x7E57u, (uint32_t)idx, (uint32_t)(idx >> 32), 0u, r0, r1, r2, r3);
     if (which == 3) {
