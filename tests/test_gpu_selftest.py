@@ -1,7 +1,7 @@
 """The kernel's exact arithmetic shortcuts against their reference form on the GPU (rt2_selftest).
 
 * div_by_inv: the unit-normal axis-aligned quad test divides by the ray's correctly rounded
-  reciprocal with two fma corrections; it must equal IEEE a / b bit for bit wherever the quad test
+  reciprocal with one fma correction; it must equal IEEE a / b bit for bit wherever the quad test
   can accept the quotient (|b| > 1e-8, a / b >= tmin).
 * aabb_hit_fin: the NaN-free slab test must decide exactly like the reference's swap +
   glm::max/min chain with early exits (AABB.hpp:34-47) for every ray with a finite inverse.
