@@ -867,9 +867,15 @@ __device__ __forceinline__ bool sphere_t_rec(float4 r0, float4 r1, f3 o, f3 d, f
   float disc = hh * hh - a * c;
   if (disc < 0.0f) return false;
   float sq = sqrtf(disc);
-  float root = (hh - sq) / a;
+  // The two roots (hh -+ sq) / a: by the correctly rounded 1/a with one fma correction
+  // (div_by_inv, equal to IEEE division for every pair of significands) when the wave's a and
+  // numerators keep its intermediates normal and finite (an accepted root >= tmin then has
+  // |num| >= 0.001 a >= 2^-70, so its correction term stays above 2^-126); IEEE division otherwise.
+  const bool fast = __all(a >= 0x1p-60f && a <= 0x1p60f && fabsf(hh) + sq <= 0x1p60f);
+  const float inv_a = fast ? rcp_nr(a) : 0.0f;
+  float root = fast ? div_by_inv(hh - sq, a, inv_a) : (hh - sq) / a;
   if (!(tmin < root && root < tmax)) {
-    root = (hh + sq) / a;
+    root = fast ? div_by_inv(hh + sq, a, inv_a) : (hh + sq) / a;
     if (!(tmin < root && root < tmax)) return false;
   }
   t_out = root;
