@@ -51,6 +51,7 @@ SALU_PEAK_GINST = 256 * MAX_CLOCK_HZ / 1e9  # 614.4 G instructions/s
 REC_BYTES = {"bvh_tests": 32, "quad_tests": 80, "sphere_tests": 32, "xform_visits": 128, "medium_tests": 16,
              "list_visits": 16}
 FLOPS = {"bvh_tests": 18, "quad_tests": 45, "sphere_tests": 30, "xform_visits": 45, "medium_tests": 20}
+GATHER_REPS = 5  # isolated gathers timed after the steps (gather_ms_per_step)
 KERNEL_SOURCES = ["raytrace2_amd/csrc/render.hip", "raytrace2_amd/csrc/rt2_layout.h", "raytrace2_amd/csrc/Makefile"]
 
 
@@ -147,14 +148,17 @@ def find_profile(key):
     return stale if stale else (best, None, False)
 
 
-def roofline_for(tr, rays_local, launches, kernel_ms, key, rank_stats_frames, spp_total):
+def roofline_for(tr, rays_local, launches, kernel_ms, key, rank_stats_frames, spp_total, steps, ms_per_step):
     """Roofline of the render kernel on this GPU: the kernel is issue bound (DESIGN.md §4 Roofline),
     on the vector pipe (VALU lane-operations per second = the VALU instructions per ray of the
-    matching PMC profile x 64 x this run's rays per launch / this run's HIP-event launch time) or on
+    matching PMC profile x 64 x this run's rays per launch / this run's launch time) or on
     the CU's one scalar unit (SALU instructions per second, same scaling); `bound` is the pipe with
     the larger fraction of its peak, and both fractions are reported (valu_frac, salu_frac).
     Also: the HBM fraction (profile traffic per ray, same scaling), the §8(d) useful-flop fraction
-    and the scene-record rate (bytes of records touched per ray / launch time, not an HBM figure)."""
+    and the scene-record rate (bytes of records touched per ray / launch time, not an HBM figure).
+    Launch time = the render kernel's GPU time per launch (rt2_stats.kernel_ms: each launch timed by
+    its own clock from its first wave to its last, overlapping launches counted once). A kernel time
+    per step above the step's wall time would be a timing fault: then no fraction is reported."""
     tr.enable_stats(True)
     tr.Reset()
     tr.reset_stats()
@@ -170,8 +174,13 @@ def roofline_for(tr, rays_local, launches, kernel_ms, key, rank_stats_frames, sp
     out = {"bound": "valu_issue", "unit": "Tlane-op/s", "peak": round(VALU_PEAK_TLANE_OPS, 2),
            "achieved": None, "frac": None, "traffic": None, "traffic_unit": "HBM bytes per launch (PMC)",
            "kernel": "rt2::dev::render_kernel<..., false>", "avg_launch_ms": round(avg_launch_s * 1e3, 3),
-           "rays_per_launch": int(rays_per_launch), "profile": src, "profile_stale": stale}
-    if prof:
+           "rays_per_launch": int(rays_per_launch), "profile": src, "profile_stale": stale,
+           "kernel_ms_per_step": round(kernel_ms / max(1, steps), 2)}
+    consistent = kernel_ms / max(1, steps) <= ms_per_step * 1.001
+    if not consistent:
+        out["invalid"] = (f"kernel time per step {kernel_ms / max(1, steps):.2f} ms exceeds the step's wall time "
+                          f"{ms_per_step:.2f} ms: no fraction reported")
+    if prof and consistent:
         pr = prof["per_ray"]
         valu = pr["valu_insts"] * rays_per_launch  # wave instructions per launch
         salu = pr.get("salu_insts", 0.0) * rays_per_launch
@@ -190,6 +199,8 @@ def roofline_for(tr, rays_local, launches, kernel_ms, key, rank_stats_frames, sp
             out["traffic"] = int(pr["hbm_bytes"] * rays_per_launch)
             out["hbm_frac"] = round(out["traffic"] / avg_launch_s / 1e9 / HBM_PEAK_GBS, 4)
         out["profile_kernel_sha"] = (prof.get("key") or {}).get("kernel_sha")
+    if not consistent:
+        return out
     out["useful_flop_frac"] = round(rays_per_launch * f_ray / avg_launch_s / 1e12 / FP32_VALU_PEAK_TFLOPS, 4)
     frame_bytes = 12 * spp_total  # the float3 sample store per (pixel, frame), per launch below
     out["record_rate_gbs"] = round((rays_per_launch * b_ray) / avg_launch_s / 1e9, 1)
@@ -351,7 +362,8 @@ def main():
             tr.set_partition(a.band_h, er, a.emulate_world)
         el, st = timed(a.steps, a.warmup)
         per_rank.append({"rank": er, "rows": tr.local_rows(), "elapsed_s": el, "rays": st["rays"],
-                         "kernel_ms": st["kernel_ms"], "launches": st["launches"], "gather_ms": st["gather_ms"],
+                         "kernel_ms": st["kernel_ms"], "launch_ms_sum": st["launch_ms_sum"], "launches": st["launches"],
+                         "gather_ms": st["gather_ms"],
                          "gathers": st["gathers"], "enqueue_ms": st.get("enqueue_ms", 0.0),
                          "readbacks": st.get("readbacks", 0), "readback_ms": st.get("readback_ms", 0.0),
                          "mray_s": st["rays"] / el / 1e6})
@@ -361,12 +373,24 @@ def main():
                 ps = tr.part_stats(g)
                 per_rank[-1]["gpus"].append({"gpu": g, "rays": ps["rays"], "kernel_ms": ps["kernel_ms"],
                                              "enqueue_ms": ps["enqueue_ms"], "launches": ps["launches"]})
-    # One gather + readback after the timed steps with the GPU otherwise idle: the event pair around
-    # a step's gather in a run of back-to-back steps also spans the time its small kernels (the
-    # RCCL gather, the de-interleave) wait for CUs behind the next step's render, whose persistent
-    # waves hold them (gather_ms_per_step); this is the cost of the exchange itself.
-    gather_iso_ms = None
+    # The exchange itself, timed on an otherwise idle GPU: in a run of back-to-back steps the gather's
+    # small kernels (the RCCL gather, the de-interleave) wait for CUs behind the next step's render,
+    # whose persistent waves hold them, so the event pair around a step's gather spans that queue time
+    # (gather_span_ms_per_step). gather_ms_per_step is the mean over GATHER_REPS isolated gathers
+    # (HIP events on the root stream around ncclGather + de-interleave); gather_readback_ms_isolated
+    # is the host wall time of one gather + NonConvertedPixels() readback.
+    gather_iso_ms = gather_ms_iso = None
     if mode in ("ranks", "multi") and host_gather is None:
+        g0 = tr.stats()
+        for _ in range(GATHER_REPS):
+            sync_all()
+            if mode == "ranks":
+                dist.barrier()
+            tr.gather()
+            sync_all()
+        g1 = tr.stats()
+        if g1["gathers"] > g0["gathers"]:
+            gather_ms_iso = (g1["gather_ms"] - g0["gather_ms"]) / (g1["gathers"] - g0["gathers"])
         sync_all()
         if mode == "ranks":
             dist.barrier()
@@ -412,7 +436,8 @@ def main():
         if mode == "multi" and n_gpus > 1:  # per-GPU share (kernel_ms is the busiest GPU's)
             gpu_rays = mine["rays"] / n_gpus
         roofline = roofline_for(tr, gpu_rays, launches, gpu_kernel_ms, key, a.stats_frames,
-                                tr.local_rows() * a.width * a.spp * a.steps // max(1, launches))
+                                tr.local_rows() * a.width * a.spp * a.steps // max(1, launches), a.steps,
+                                mine["elapsed_s"] * 1e3 / a.steps)
         if not a.no_cpu:
             cpu = cpu_baseline(a, scene_file)
 
@@ -459,7 +484,9 @@ def main():
             "detail": {"rays": int(rays_total), "launches": me["launches"], "setup_s": round(setup_s, 3),
                        "kernel_sha": key["kernel_sha"], "source_kernel_sha": src_sha,
                        "kernel_ms_per_step_max": round(max(r["kernel_ms"] for r in per_rank) / a.steps, 2),
-                       "gather_ms_per_step": round(per_rank[0]["gather_ms"] / a.steps, 3),
+                       "launch_ms_sum_per_step": round(per_rank[0]["launch_ms_sum"] / a.steps, 2),
+                       "gather_ms_per_step": None if gather_ms_iso is None else round(gather_ms_iso, 3),
+                       "gather_span_ms_per_step": round(per_rank[0]["gather_ms"] / a.steps, 3),
                        "gather_readback_ms_isolated": gather_iso_ms,
                        "readback_ms_per_step": round(per_rank[0]["readback_ms"] / a.steps, 3),
                        "readback_bytes_per_step": (a.width * a.height * 12 if per_rank[0]["readbacks"] else 0),

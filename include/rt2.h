@@ -228,7 +228,10 @@ typedef struct {
   uint64_t bvh_tests, quad_tests, sphere_tests, xform_visits, medium_tests, list_visits;
   uint64_t overflow;  /* lanes that hit the traversal-stack bound (must be 0) */
   uint64_t launches;
-  double kernel_ms;   /* sum of per-launch HIP event durations */
+  /* render-kernel GPU time: the time in which at least one render launch ran, each launch timed by
+   * its own clock from its first wave's start to its last wave's end (queue time excluded;
+   * consecutive launches overlap in the previous launch's tail, counted once) */
+  double kernel_ms;
   uint64_t stamps[4]; /* diagnostic builds only: s_memtime sums (fetch, trace, shade, finish) */
   uint64_t diag[8];   /* diagnostic builds only: per-wave traversal step counts */
   /* multi-GPU (root): gathers done, and the sum of their root-stream durations (HIP events from the
@@ -245,6 +248,9 @@ typedef struct {
   /* times the library blocked the host on the GPU (stream / event synchronizations); the launch path
    * (Render, flush, gather, the async readbacks) adds none */
   uint64_t host_waits;
+  /* the sum of the render launches' first-wave-to-last-wave times (>= kernel_ms: overlaps counted
+   * once per launch) */
+  double launch_ms_sum;
 } rt2_stats;
 RT2_API int rt2_tracer_get_stats(rt2_tracer* tr, rt2_stats* out);
 /* The stats of GPU `part` of a multi-GPU tracer (part 0 of a one-GPU tracer is itself). */

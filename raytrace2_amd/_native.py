@@ -62,7 +62,8 @@ class Stats(ctypes.Structure):
                                                                            ("enqueue_ms", ctypes.c_double),
                                                                            ("readbacks", ctypes.c_uint64),
                                                                            ("readback_ms", ctypes.c_double),
-                                                                           ("host_waits", ctypes.c_uint64)]
+                                                                           ("host_waits", ctypes.c_uint64),
+                                                                           ("launch_ms_sum", ctypes.c_double)]
 
     def as_dict(self):
         d = {n: (getattr(self, n) if n.endswith("_ms") else int(getattr(self, n))) for n, _ in self._fields_
@@ -164,8 +165,15 @@ def _load():
         "rt2_deinterleave_host": (i32, [fp, fp, i32, i32, i32, i32, i32, i32]),
         "rt2_runtime_info": (i32, [ctypes.c_char_p, ctypes.c_size_t]),
     }
+    # RT2_ALLOW_OLD_LIB=1 (tools/ A/B runs of earlier builds only): entry points the older library lacks
+    # are left out; otherwise a library that does not export every entry point is a load error
+    allow_old = os.environ.get("RT2_ALLOW_OLD_LIB") == "1"
+    missing = [name for name in sig if not hasattr(L, name)]
+    if missing and not allow_old:
+        raise ImportError(f"raytrace2_amd: {LIB_PATH} does not export {missing} (a stale build? rebuild with "
+                          f"make -C raytrace2_amd/csrc)")
     for name, (res, args) in sig.items():
-        if not hasattr(L, name):  # an older library (tools/ A/B runs of earlier builds): absent entry points
+        if name in missing:
             continue
         fn = getattr(L, name)
         fn.restype = res
@@ -193,6 +201,8 @@ def selftest(which: int, n: int, seed: int = 1, device: int = 0):
 def multi_plan(n_gpus: int, devices=None, band_h: int = 0, width: int = 0, height: int = 0):
     """rt2_multi_plan: rt2_tracer_create_multi's argument checks and per-GPU partition, on the host
     (no GPU, no RCCL). Returns (list of part dicts, loopback)."""
+    if devices is not None and len(devices) != n_gpus:
+        raise ValueError(f"multi_plan: {len(devices)} device ids for n_gpus = {n_gpus}")
     plans = (PartPlan * max(1, n_gpus))()
     devs = (ctypes.c_int * len(devices))(*devices) if devices is not None else None
     lb = ctypes.c_int(0)

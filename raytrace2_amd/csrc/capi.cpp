@@ -131,8 +131,19 @@ struct rt2_tracer {
   int last_grid = 0;
   uint64_t launches = 0;
   uint64_t paths = 0;
+  // Render-kernel time, from the launches' own clocks (RenderParams::launch_clock): a ring of
+  // kClockRing (start complement, end) pairs on the device, read back at the next synchronization.
+  // kernel_ms is the time at least one render launch of this tracer ran (the union of the launches'
+  // first-wave-to-last-wave intervals: consecutive launches overlap in a launch's tail);
+  // launch_ms_sum adds the intervals up (the overlap counted twice).
   double kernel_ms = 0;
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;  // per-launch timing events
+  double launch_ms_sum = 0;
+  unsigned long long* d_clock = nullptr;  // [kClockRing][2]
+  unsigned long long* h_clock = nullptr;  // pinned copy
+  uint32_t clock_next = 0;                // next ring entry
+  std::vector<uint32_t> pending;          // ring entries of launches not yet read back
+  double clock_khz = 100000.0;            // hipDeviceAttributeWallClockRate
+  unsigned long long busy_end = 0;        // end of the union so far (clock ticks)
   std::vector<hipEvent_t> event_pool;
   // ---- multi-GPU ----
   std::vector<rt2_tracer*> parts;  // multi tracer: one one-GPU tracer per device, parts[i] = rank i
@@ -270,13 +281,26 @@ hipEvent_t TakeEvent(rt2_tracer* t) {
 
 int DrainEvents(rt2_tracer* t) {
   if (!t->pending.empty() || !t->gpending.empty() || !t->rpending.empty()) t->host_waits++;
-  for (auto& pr : t->pending) {
-    HIP_TRY(hipEventSynchronize(pr.second));
-    float ms = 0;
-    HIP_TRY(hipEventElapsedTime(&ms, pr.first, pr.second));
-    t->kernel_ms += ms;
-    t->event_pool.push_back(pr.first);
-    t->event_pool.push_back(pr.second);
+  if (!t->pending.empty()) {
+    // every render launch is followed by its accumulate on the tracer stream, so a copy queued there
+    // reads the clocks of all of them
+    HIP_TRY(hipSetDevice(t->device));
+    HIP_TRY(hipMemcpyAsync(t->h_clock, t->d_clock, 2 * sizeof(unsigned long long) * kClockRing,
+                           hipMemcpyDeviceToHost, t->stream));
+    HIP_TRY(hipStreamSynchronize(t->stream));
+    std::vector<std::pair<unsigned long long, unsigned long long>> iv;
+    for (uint32_t k : t->pending) {
+      const unsigned long long s = ~t->h_clock[2 * k], e = t->h_clock[2 * k + 1];
+      if (t->h_clock[2 * k] != 0ull && e >= s) iv.emplace_back(s, e);
+    }
+    std::sort(iv.begin(), iv.end());
+    const double ms_per_tick = 1.0 / t->clock_khz;
+    for (const auto& x : iv) {
+      t->launch_ms_sum += (double)(x.second - x.first) * ms_per_tick;
+      const unsigned long long from = std::max(x.first, t->busy_end);
+      if (x.second > from) t->kernel_ms += (double)(x.second - from) * ms_per_tick;
+      t->busy_end = std::max(t->busy_end, x.second);
+    }
   }
   t->pending.clear();
   for (auto& pr : t->gpending) {
@@ -555,6 +579,14 @@ int rt2_tracer_create(const rt2_scene* s, int device, rt2_tracer** out) {
     t->lin_len = (uint32_t)(c.lin.size() / 4);
   }
   HIP_TRY(hipMalloc(&t->d_work, 128));
+  HIP_TRY(hipMalloc(&t->d_clock, 2 * sizeof(unsigned long long) * kClockRing));
+  HIP_TRY(hipMemset(t->d_clock, 0, 2 * sizeof(unsigned long long) * kClockRing));
+  HIP_TRY(hipHostMalloc((void**)&t->h_clock, 2 * sizeof(unsigned long long) * kClockRing, hipHostMallocDefault));
+  {
+    int khz = 0;  // the constant clock s_memrealtime counts (100 MHz on MI355X)
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) == hipSuccess && khz > 0)
+      t->clock_khz = (double)khz;
+  }
   HIP_TRY(hipMalloc(&t->d_stats, kStatsSlots * sizeof(unsigned long long)));
   HIP_TRY(hipMemset(t->d_stats, 0, kStatsSlots * sizeof(unsigned long long)));
   t->root = c.root;
@@ -609,11 +641,9 @@ void rt2_tracer_destroy(rt2_tracer* t) {
     (void)hipEventDestroy(pr.second);
   }
   if (t->stream) (void)hipStreamSynchronize(t->stream);
-  for (auto& pr : t->pending) {
-    (void)hipEventDestroy(pr.first);
-    (void)hipEventDestroy(pr.second);
-  }
   for (hipEvent_t e : t->event_pool) (void)hipEventDestroy(e);
+  (void)hipFree(t->d_clock);
+  if (t->h_clock) (void)hipHostFree(t->h_clock);
   FreeFrame(t);
   (void)hipFree(t->d_nodes);
   (void)hipFree(t->d_materials);
@@ -1129,11 +1159,13 @@ int LaunchFrames(rt2_tracer* t, int n_frames) {
     t->last_chunk_frames = L.first_len;
     p.work_counter = t->d_work + 16 * (&sl - t->slots);
     HIP_TRY(hipMemsetAsync(p.work_counter, 0, sizeof(uint32_t), sl.stream));
-    hipEvent_t e0 = TakeEvent(t), e1 = TakeEvent(t);
-    if (e0) HIP_TRY(hipEventRecord(e0, sl.stream));
+    // the launch's clock pair (RenderParams::launch_clock; read back by DrainEvents)
+    const uint32_t ck = t->clock_next;
+    t->clock_next = (t->clock_next + 1u) % (uint32_t)kClockRing;
+    p.launch_clock = t->d_clock + 2u * ck;
+    HIP_TRY(hipMemsetAsync(p.launch_clock, 0, 2 * sizeof(unsigned long long), sl.stream));
     HIP_TRY(LaunchRender(p, variant, counting, grid, sl.stream));
-    if (e1) HIP_TRY(hipEventRecord(e1, sl.stream));
-    if (e0 && e1) t->pending.emplace_back(e0, e1);
+    t->pending.push_back(ck);
     // accumulate in frame order on the tracer stream, after this launch (RayTracer.cpp:64)
     HIP_TRY(hipEventRecord(sl.rendered, sl.stream));
     HIP_TRY(hipStreamWaitEvent(t->stream, sl.rendered, 0));
@@ -1144,8 +1176,12 @@ int LaunchFrames(rt2_tracer* t, int n_frames) {
     t->launches++;
     t->paths += (uint64_t)p.n_frames * p.local_pixels;
     t->frame_idx += p.n_frames;
+    // the ring's entries of unread launches must not be reused: read them back at half the ring
+    if (t->pending.size() >= (size_t)kClockRing / 2) {
+      int rc2 = DrainEvents(t);
+      if (rc2 != RT2_OK) return rc2;
+    }
   }
-  if (t->pending.size() > 256) return DrainEvents(t);
   return RT2_OK;
 }
 
@@ -1516,6 +1552,7 @@ int rt2_tracer_get_stats(rt2_tracer* t, rt2_stats* o) {
       sum.overflow += s.overflow;
       sum.launches = std::max(sum.launches, s.launches);
       sum.kernel_ms = std::max(sum.kernel_ms, s.kernel_ms);
+      sum.launch_ms_sum = std::max(sum.launch_ms_sum, s.launch_ms_sum);
       for (int k = 0; k < 4; k++) sum.stamps[k] += s.stamps[k];
       for (int k = 0; k < 8; k++) sum.diag[k] += s.diag[k];
       sum.gathers += s.gathers;
@@ -1548,6 +1585,7 @@ int rt2_tracer_get_stats(rt2_tracer* t, rt2_stats* o) {
   for (int k = 0; k < 8; k++) o->diag[k] = s[StatsCounters::kDiag + k];
   o->launches = t->launches;
   o->kernel_ms = t->kernel_ms;
+  o->launch_ms_sum = t->launch_ms_sum;
   o->gathers = t->gathers;
   o->gather_ms = t->gather_ms;
   o->enqueue_ms = t->enqueue_ms;
@@ -1740,6 +1778,8 @@ int rt2_tracer_reset_stats(rt2_tracer* t) {
   t->launches = 0;
   t->paths = 0;
   t->kernel_ms = 0;
+  t->launch_ms_sum = 0;
+  t->busy_end = 0;
   t->gathers = 0;
   t->gather_ms = 0;
   t->enqueue_ms = 0;

@@ -80,36 +80,6 @@ constexpr int kBlock = 256;
 #ifndef RT2_MIN_WAVES_ALL
 #define RT2_MIN_WAVES_ALL 6
 #endif
-#ifndef RT2_BOX_PAIR
-#define RT2_BOX_PAIR 1
-#endif
-#ifndef RT2_PARK
-#define RT2_PARK 1
-#endif
-#ifndef RT2_STAGE
-#define RT2_STAGE 1  // 0: samples written with plain 12-B stores (no LDS staging)
-#endif
-#ifndef RT2_BVH_SELECT
-#define RT2_BVH_SELECT 1  // lockstep BVH steps: lanes take the step's result by a select, no branch
-#endif
-#ifndef RT2_PHILOX_RK
-#define RT2_PHILOX_RK 1  // path-stream Philox round keys precomputed on the host (philox_path)
-#endif
-#ifndef RT2_WORLD_NORMAL
-#define RT2_WORLD_NORMAL 1  // transformed QUADAA quads carry their world normal (compile.cpp WorldNormal)
-#endif
-#ifndef RT2_XRAY
-#define RT2_XRAY 1  // the Cornell kernel keeps the hit's model-space ray from the trace (resolve_hit)
-#endif
-#ifndef RT2_STAGE_RING
-#define RT2_STAGE_RING 0  // 1: the ring kernels stage samples in LDS too
-#endif
-#ifndef RT2_RNG_RING
-#define RT2_RNG_RING 1
-#endif
-#ifndef RT2_KEEP_WINV
-#define RT2_KEEP_WINV 1
-#endif
 #ifndef RT2_MIN_WAVES_PER_EU
 #define RT2_MIN_WAVES_PER_EU 0  // 0: per-variant occupancy targets (kMinWaves below)
 #endif
@@ -425,7 +395,7 @@ __device__ __forceinline__ void philox(uint32_t k0, uint32_t k1, uint32_t pixel,
 template <bool kRK>
 __device__ __forceinline__ void philox_path(uint32_t pixel, uint32_t frame, uint32_t block, uint32_t& r0,
                                             uint32_t& r1, uint32_t& r2, uint32_t& r3) {
-  if constexpr (!(RT2_PHILOX_RK && kRK)) {
+  if constexpr (!kRK) {
     uint32_t key0, key1;
     seed_args(key0, key1);
     philox(key0, key1, pixel, frame, block, r0, r1, r2, r3);
@@ -1166,41 +1136,6 @@ __device__ __forceinline__ bool quad_aa_div(const uint32_t* r, f3 o, f3 d, float
   t_out = t;
   return (int)!(fabsf(dk) <= 1e-8f) & (int)unit_pair(alpha, beta);
 }
-// The words come two quads (one 64-byte scalar load) at a time: no dependent loads, few SGPRs.
-__device__ __forceinline__ bool boundary_aa(const void* recs, uint32_t off, uint32_t hdr, f3 o, f3 d, float lo,
-                                            float hi, float& t_out, Counters& cnt) {
-  const uint32_t n = (hdr >> 24) & 7u;
-  bool any = false;
-  for (uint32_t k = 0; k < n; k += 2u) {  // wave-uniform
-    const u32x16 w = sld16(recs, off + 32u * k);
-#pragma unroll
-    for (uint32_t j = 0; j < 2u; j++) {
-      if (k + j < n) {
-        uint32_t r[8];
-#pragma unroll
-        for (int i = 0; i < 8; i++) r[i] = w[8 * j + i];
-        const uint32_t code = (hdr >> (3u * (k + j))) & 7u;
-        float t;
-        bool ok;
-        if (code == 0u) {
-          ok = quad_aa_div<0>(r, o, d, t);
-        } else if (code == 1u) {
-          ok = quad_aa_div<1>(r, o, d, t);
-        } else {
-          ok = quad_aa_div<2>(r, o, d, t);
-        }
-        cnt.quad++;
-        if (ok & (lo <= t) & (t <= hi)) {
-          any = true;
-          hi = t;
-        }
-      }
-    }
-  }
-  if (any) t_out = hi;
-  return any;
-}
-
 // Both boundary queries of ConstantMedium::Hit (ConstantMedium.cpp:14-58) on a box in one pass:
 // each quad's t and interior decision do not depend on the query's interval, so its quads are
 // tested once and the two answers selected from the candidates — t1 = the smallest candidate in
@@ -1262,12 +1197,7 @@ __device__ __forceinline__ bool medium_t_lin(const void* recs, uint32_t moff, co
   // a box (the sphere scenes' kernels keep the general path: the 48 words cost them SGPRs)
   if (!Has<F, kFeatSphere>() && (r0.w & kBoundaryAAFlag)) {
     const uint32_t off = (moff + 1u) * 16u;
-#if RT2_BOX_PAIR
     if (!boundary_aa_pair(recs, off, r0.w, o, d, t1, t2, cand, cnt)) return false;
-#else
-    if (!boundary_aa(recs, off, r0.w, o, d, -FLT_MAX, FLT_MAX, t1, cnt)) return false;
-    if (!boundary_aa(recs, off, r0.w, o, d, (float)((double)t1 + 0.0001), FLT_MAX, t2, cnt)) return false;
-#endif
   } else {
 #if RT2_EXP_TWICE & 128
   {
@@ -1490,9 +1420,9 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
                                              lds_u32* cand, lds_u32* xray, Counters& cnt) {
   const Nodes<kModeLinear> N{reinterpret_cast<const float4*>(P.lind)};  // boundaries / nested xforms
   const void* recs = P.lind;
-  // the world ray's reciprocal is recomputed where a transform's exit returns to world space
-  // (RT2_KEEP_WINV keeps it in registers: three VGPRs live across the whole trace)
-  constexpr bool kKeepW = RT2_KEEP_WINV && !__is_same(W, ParkRay);
+  // the world ray's reciprocal stays in registers for the transforms' exits to world space (three
+  // VGPRs live across the trace), except with the parked ray (book 2), which recomputes it there
+  constexpr bool kKeepW = !__is_same(W, ParkRay);
   f3 o = wray.wo(), d = wray.wd();
   f3 inv = recip3(d);
   const f3 winv = inv;
@@ -1527,7 +1457,7 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
         // kSel: every lane evaluates the step (the same VALU issue: masked lanes cost their slots
         // anyway) and the lanes at it take the result by a select, no exec-mask branch per step
         // (Cornell +0.4 %; the sphere kernels keep the branch: book 1 -0.4 % with the select)
-        constexpr bool kSel = RT2_BVH_SELECT && !Has<F, kFeatSphere>();
+        constexpr bool kSel = !Has<F, kFeatSphere>();
         const bool act = next == i;
         if (kSel || act) {
           if (kStats && act) cnt.bvh++;
@@ -1813,7 +1743,6 @@ __device__ __forceinline__ void resolve_hit(const Nodes<kMode>& N, const HitRef&
     f3 qn = xyz(N[off + 2]);
     front = dot(d, qn) < 0.0f;
     n = front ? qn : -qn;
-#if RT2_WORLD_NORMAL
     const float4 r3 = N[off + 3];
     mat = bits(r3.w);
     if (Has<F, kFeatXform>() && h.xf != kRefNone) {
@@ -1823,9 +1752,6 @@ __device__ __forceinline__ void resolve_hit(const Nodes<kMode>& N, const HitRef&
       n = front ? wn : -wn;
       wnormal = true;
     }
-#else
-    mat = N.word(off + 3, 3);
-#endif
   } else {
     f3 qn = xyz(N[off]);
     front = dot(d, qn) < 0.0f;
@@ -2018,20 +1944,20 @@ constexpr bool LdsRng() {
 template <uint32_t F, int kMode, bool kStats>
 constexpr bool Park() {
   constexpr uint32_t kBook2 = kFeatSphere | kFeatMedium | kFeatXform | kFeatNoise | kFeatSpecular | kFeatAccList;
-  return RT2_PARK && F == kBook2 && kMode == kModeLinear && !kStats && LdsRng<F, kMode, kStats>();
+  return F == kBook2 && kMode == kModeLinear && !kStats && LdsRng<F, kMode, kStats>();
 }
 // Kernels whose threaded medium step takes both box-boundary queries in one pass (boundary_aa_pair):
 // their LDS holds the candidates.
 template <uint32_t F, int kMode>
 constexpr bool BoxPair() {
-  return RT2_BOX_PAIR && kMode == kModeLinear && Has<F, kFeatMedium>() && !Has<F, kFeatSphere>();
+  return kMode == kModeLinear && Has<F, kFeatMedium>() && !Has<F, kFeatSphere>();
 }
 
 // Kernels with the two-block Philox ring (PathT kRing): 8 Philox planes, where the LDS room allows it (not
 // beside the Cornell volume kernel's candidate planes or book 2's park planes).
 template <uint32_t F, int kMode, bool kStats>
 constexpr bool Ring() {
-  return RT2_RNG_RING && LdsRng<F, kMode, kStats>() && !Park<F, kMode, kStats>() && !BoxPair<F, kMode>();
+  return LdsRng<F, kMode, kStats>() && !Park<F, kMode, kStats>() && !BoxPair<F, kMode>();
 }
 template <uint32_t F, int kMode, bool kStats>
 constexpr uint32_t StageGroup() {
@@ -2039,7 +1965,7 @@ constexpr uint32_t StageGroup() {
   // the ring kernels (Cornell, book 1) store samples directly: their staging logic cost more time than
   // the write traffic it saves (round 4, same box: C2 +0.9 %, book 1 +1 %; 12-B stores write the
   // octets' sectors partially, about 3x the sample bytes, 2.5 % of HBM bandwidth at the headline)
-  if (!RT2_STAGE || (RT2_STAGE_RING == 0 && Ring<F, kMode, kStats>())) return 0u;
+  if (Ring<F, kMode, kStats>()) return 0u;
   // octets need 5.25 KB per wave: with the LDS Philox blocks beside them they fit no occupancy >= 7
   return MinWaves<F, kMode, kStats>() <= 7 && !LdsRng<F, kMode, kStats>() ? 8u : 4u;
 }
@@ -2066,7 +1992,7 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
   constexpr uint32_t kParkP = kCandP + (BoxPair<F, kMode>() ? kBoundaryAAMax : 0u);
   // the model-space ray of the transform holding the closest hit, kept by the trace for resolve_hit
   // (the ring kernels with transforms: the Cornell box)
-  constexpr bool kXray = RT2_XRAY && Ring<F, kMode, kStats>() && Has<F, kFeatXform>();
+  constexpr bool kXray = Ring<F, kMode, kStats>() && Has<F, kFeatXform>();
   constexpr uint32_t kXrayP = kParkP + (kPark ? (uint32_t)kParkWords : 0u);
   constexpr uint32_t kWavePlanes = kXrayP + (kXray ? 6u : 0u);
   lds_u32* lp = nullptr;  // this lane's word of plane 0
@@ -2095,6 +2021,8 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
   uint32_t dl = 0;
   Counters cnt = {};
   bool overflow = false;
+  // the launch's first-wave start (RenderParams::launch_clock; minimum as the maximum of complements)
+  if (lane == 0 && P.launch_clock != nullptr) atomicMax(P.launch_clock, ~__builtin_amdgcn_s_memrealtime());
 #if RT2_EXP_ENDTIME
   const unsigned long long et_start = __builtin_amdgcn_s_memrealtime();
   unsigned long long et_idle = 0;  // first loop head at which a lane of this wave found no work
@@ -2480,6 +2408,8 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
     atomicAdd(P.stats + StatsCounters::kListVisits, (unsigned long long)cnt.list);
   }
   if (overflow) atomicAdd(P.stats + StatsCounters::kCount, 1ull);  // overflow flag slot
+  // the launch's last-wave end
+  if (lane == 0 && P.launch_clock != nullptr) atomicMax(P.launch_clock + 1, __builtin_amdgcn_s_memrealtime());
 #if RT2_EXP_WAVESTEPS
   for (int k = 0; k < 8; k++) atomicAdd(P.stats + StatsCounters::kDiag + k, (unsigned long long)cnt.wd[k]);
 #endif

@@ -268,6 +268,13 @@ struct RenderParams {
   // for rounds r = 0..9, interleaved (the kernel loads them with two scalar loads per block instead
   // of computing 18 adds on the scalar unit at every refill)
   uint32_t philox_keys[20];
+  // This launch's clock pair (capi.cpp launch-clock ring, zeroed before the launch): word 0 = the
+  // largest complement of a wave's start time (so ~word 0 is the first wave's start), word 1 = the
+  // last wave's end, in ticks of the GPU's constant 100 MHz clock (s_memrealtime). A launch's GPU
+  // time is then measured from its first wave to its last one, whatever it waited for in its queue
+  // (with two launch slots the next launch is queued while the previous one still holds the CUs).
+  unsigned long long* launch_clock;
 };
+constexpr int kClockRing = 512;  // launch-clock pairs per tracer (drained at half)
 
 }  // namespace rt2

@@ -120,3 +120,8 @@ def test_multi_plan_rejects_bad_arguments():
     for args in [(0, None), (3, [0, 1, 1]), (2, [0, -1]), (2, [0, 1], -1)]:
         with pytest.raises(Rt2Error):
             multi_plan(*args)
+    # a device list of another length than n_gpus is refused before the C call (the C
+    # side reads n_gpus entries)
+    for n, devs in [(3, [0, 1]), (1, [0, 1])]:
+        with pytest.raises(ValueError):
+            multi_plan(n, devs)

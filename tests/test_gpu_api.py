@@ -51,3 +51,35 @@ def test_queued_frames_and_reset(tracer):
     tracer.Render(3)
     a = tracer.Accumulation()
     assert tracer.FrameIdx() == 3 and a.any()
+
+
+def test_kernel_time_is_gpu_busy_time_not_queue_time(have_gpu):
+    """with two launch slots, step i + 1's render is queued while step i's still
+    holds the CUs; kernel_ms must count the time the GPU ran render launches (each launch timed by its
+    own first-wave / last-wave clock, overlaps once), not the time a launch waited in its queue. Back
+    to back renders (the bench's step shape, no host wait between them): kernel time <= wall time,
+    the sum of the launches' own times >= their union, and the GPU-bound run is mostly kernel time."""
+    import time
+    sc = R.Scene(scene_path("cornell_box_original"), R.DEFAULT_SEED)
+    tr = R.RayTracer(sc, 0)
+    tr.SetSamplesPerPixel(1000)
+    tr.OnResize((256, 256))
+    tr.Render(100)
+    tr.synchronize()
+    tr.reset_stats()
+    steps = 6
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        tr.Reset()
+        tr.Render(1000)
+        tr.flush()
+    tr.synchronize()
+    wall_ms = (time.perf_counter() - t0) * 1e3
+    st = tr.stats()
+    tr.close()
+    assert st["launches"] == steps
+    assert 0.0 < st["kernel_ms"] <= wall_ms * 1.001, (st["kernel_ms"], wall_ms)
+    assert st["launch_ms_sum"] >= st["kernel_ms"] * 0.9999, (st["launch_ms_sum"], st["kernel_ms"])
+    # consecutive launches overlap only in a launch's tail (about a millisecond)
+    assert st["launch_ms_sum"] <= st["kernel_ms"] + 3.0 * steps, (st["launch_ms_sum"], st["kernel_ms"])
+    assert st["kernel_ms"] >= 0.6 * wall_ms, (st["kernel_ms"], wall_ms)
