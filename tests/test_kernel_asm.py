@@ -111,3 +111,72 @@ def test_book2_bench_kernel_spills_stay_out_of_the_trace(isa):
     scratch, body = _kernel(isa, "ILj303ELi2ELb0E")
     deep = [x for x in _loop_depth_scratch(body) if x[0] >= 2]
     assert scratch <= 96 and not deep, (scratch, deep[:5])
+
+
+def _loops(body):
+    """Every loop of a kernel body: (header label, depth, opcode counts of the loop's blocks)."""
+    import collections
+    blocks, cur = [], None
+    for line in body.split("\n"):
+        if line.startswith(".LBB") or line.startswith("; %bb"):
+            cur = [line.split()[0].rstrip(":") if line.startswith(".LBB") else line.split()[1], [line], []]
+            blocks.append(cur)
+        elif cur is not None and line.strip().startswith(";"):
+            if not cur[2]:
+                cur[1].append(line)
+        elif cur is not None and line.startswith("\t") and not line.strip().startswith("."):
+            cur[2].append(line.split()[0])
+    out = []
+    for b in blocks:
+        m = re.search(r"Loop Header: Depth=(\d+)", " ".join(b[1]))
+        if not m:
+            continue
+        h = b[0].lstrip(".L")
+        c = collections.Counter()
+        for bb in blocks:
+            txt = " ".join(bb[1])
+            if bb is b or f"Header={h} " in txt or f"Parent Loop {h} " in txt or txt.endswith(f"Header={h}"):
+                c.update(bb[2])
+        out.append((b[0], int(m.group(1)), c))
+    return out
+
+
+def _salu(c):
+    return sum(v for k, v in c.items()
+               if k.startswith("s_") and not k.startswith(("s_load", "s_waitcnt", "s_nop", "s_cbranch", "s_branch")))
+
+
+def test_cornell_quad_run_loop_keeps_the_scalar_issue_code_generation(isa):
+    """+19 % of the headline rests on two LLVM options (Makefile HIPFLAGS:
+    -structurizecfg-skip-uniform-regions keeps the traversal's wave-uniform branches plain scalar
+    branches; -simplifycfg-sink-common=false keeps the three per-axis QUADAA bodies apart instead of one
+    body fed by register copies). A toolchain that silently changed what they do would cost ~16 % with
+    every other test green; this guard fails instead. The Cornell kernel's quad-run loop (the depth-3 loop
+    of the QUADAA test: the float-bit interior test's v_max_u32) must hold three separate interior tests
+    (one per axis), no exec-mask save per quad, and at most 36 SALU instructions (with the options: 30;
+    without them: 50 and one merged body); its trace loop at most 165 SALU (147; without: 190)."""
+    _, body = _kernel(isa, "ILj4ELi2ELb0E")
+    loops = _loops(body)
+    quad = [(h, c) for h, d, c in loops if d == 3 and c["v_max_u32_e32"] + c["v_max_u32_e64"] > 0 and
+            any(k.startswith("s_load") for k in c)]
+    assert len(quad) == 1, [(h, d) for h, d, _ in loops]
+    _, c = quad[0]
+    umax = c["v_max_u32_e32"] + c["v_max_u32_e64"]
+    assert umax == 3, ("per-axis QUADAA bodies merged", umax)
+    assert c["s_and_saveexec_b64"] == 0, c["s_and_saveexec_b64"]
+    assert _salu(c) <= 36, _salu(c)
+    trace = [c for h, d, c in loops if d == 2 and _salu(c) > 60]
+    assert len(trace) == 1 and _salu(trace[0]) <= 165, [_salu(c) for c in trace]
+
+
+@pytest.mark.parametrize("define", ["RT2_EXP_TRACE_TWICE=1", "RT2_EXP_TWICE=4095", "RT2_EXP_WAVESTEPS=1",
+                                    "RT2_EXP_STAMPS=1", "RT2_EXP_ENDTIME=1", "RT2_EXP_NOSTORE=1"])
+def test_diagnostic_builds_compile(define, tmp_path):
+    """The only #if sides left in render.hip are the tools/ diagnostic builds (cost probes, wave-step
+    counts, section stamps, launch-tail times, no-store traffic split): each compiles
+    for the Cornell and book 2 kernels (RT2_ONLY_VARIANT: one threaded kernel per build)."""
+    for v in (0, 3):
+        r = subprocess.run(["/opt/rocm/bin/hipcc", *makefile_hipflags(), "--cuda-device-only", "-c", "-o",
+                            str(tmp_path / f"k{v}.o"), f"-DRT2_ONLY_VARIANT={v}", f"-D{define}", SRC],
+                           capture_output=True, text=True)
+        assert r.returncode == 0, (define, v, r.stderr[-2000:])
