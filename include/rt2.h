@@ -264,7 +264,11 @@ RT2_API int rt2_tracer_reset_stats(rt2_tracer* tr);
  * 2^-100; which 4: the accelerated-list padded slab test culls no box the exact padded slab accepts,
  * zero direction components included; which 5: the reciprocal without range scaling for every float
  * bit pattern below n, n = 2^32 for all of them; which 6: division by a correctly rounded reciprocal
- * for the first n pairs of significands, n = 2^46 for all of them). Writes the number of mismatches and of inputs checked. */
+ * for the first n pairs of significands, n = 2^46 for all of them; which 7: the same for every
+ * numerator significand against n / 2^23 divisor significands each; which 8: sphere roots by the
+ * reciprocal against IEEE division on rays from near a sphere's surface, `checked` = the admitted
+ * inputs whose smaller numerator cancelled; which 9: the square root without range scaling at the
+ * samplers' inputs for every 24-bit uniform, n = 2^24). Writes the number of mismatches and of inputs checked. */
 RT2_API int rt2_selftest(int device, int which, uint64_t n, uint64_t seed, uint64_t* mismatches, uint64_t* checked);
 
 /* ---- util::WriteImage (Util.cpp:39-79): sqrt gamma, clamp(x*255.999), vertical flip ---- */

@@ -1751,7 +1751,7 @@ int rt2_tracer_image_pixels(rt2_tracer* t, uint8_t* out) {
 
 int rt2_selftest(int device, int which, uint64_t n, uint64_t seed, uint64_t* mismatches, uint64_t* checked) {
   if (!mismatches || !checked) return Fail(RT2_ERR_INVALID, "null argument");
-  if (which < 0 || which > 6) return Fail(RT2_ERR_INVALID, "unknown self-test");
+  if (which < 0 || which > 9) return Fail(RT2_ERR_INVALID, "unknown self-test");
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return Fail(RT2_ERR_HIP, "no HIP device available");
   HIP_TRY(hipSetDevice(device));

@@ -465,6 +465,31 @@ struct Flattener {
     lin[4 * me + 1] = (uint32_t)(lin.size() / 4);
     return true;
   }
+  // A transform about the y axis (every scene transform of the reference's files: ParseTransform's
+  // rotation is angleAxis about a y axis, Serialize.cpp:106-132): the off-pattern entries of M^-1 and
+  // of M (col0.y, col1.x, col1.z, col2.y) are exactly +-0, so each of their products with a finite
+  // coordinate is a +-0 summand, and the kernel leaves them out (rt2_layout.h kXformYAxis). A +-0
+  // summand changes a sum only when every other summand is zero too, and then only the sign of the
+  // zero; a zero's sign reaches no decision and no nonzero value of the path (DESIGN.md §4
+  // "Transforms about y"). The coordinates must be finite (0 * inf is NaN): the scene and the
+  // transformed object lie within +-2^100, so every ray origin (the camera, a hit point) is finite.
+  bool YAxisPattern(int i, const std::vector<float>& lind, uint32_t off) const {
+    const float* r = &lind[4 * (size_t)off];
+    for (int c : {0, 4}) {  // M^-1 (records 0-3), M (records 4-7)
+      const float* m = r + 4 * c;
+      if (!(m[1] == 0.0f && m[4] == 0.0f && m[6] == 0.0f && m[9] == 0.0f)) return false;
+      for (int k = 0; k < 12; k += 4)  // (the 3x3 part: its products stay finite)
+        for (int j = 0; j < 3; j++)
+          if (!(std::fabs(m[k + j]) <= 0x1p10f)) return false;
+    }
+    auto inside = [](const AABB& b) {
+      const float lim = 0x1p100f;
+      return std::fabs(b.x.min) <= lim && std::fabs(b.x.max) <= lim && std::fabs(b.y.min) <= lim &&
+             std::fabs(b.y.max) <= lim && std::fabs(b.z.min) <= lim && std::fabs(b.z.max) <= lim;
+    };
+    const Obj& o = s.objs[(size_t)i];
+    return inside(o.aabb) && inside(s.objs[(size_t)o.child].aabb) && inside(s.objs[(size_t)s.root].aabb);
+  }
   bool ContainsAccList(int i) const {
     const Obj& o = s.objs[(size_t)i];
     if (o.kind == kList && acc_depth.count(i)) return true;
@@ -517,6 +542,7 @@ struct Flattener {
       case kXform: {
         uint32_t off = CopyRecords(src, kXformRecords, lind);
         lind[4 * (off + 1) + 3] = Bits(parent_xf);
+        lind[4 * (off + 2) + 3] = Bits(YAxisPattern(i, lind, off) ? kXformYAxis : 0u);
         uint32_t self = make_ref(kXform, off);
         if (xf_depth >= kLinearMaxXformDepth) return false;  // the kernel nests one loop per level
         size_t me = emit(kXform, off, 0);

@@ -136,6 +136,18 @@ __device__ __forceinline__ f3 recip3(f3 d) {
     return mk(rcp_nr(d.x), rcp_nr(d.y), rcp_nr(d.z));
   return mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
 }
+// recip3 of a normalize result (every component is a NaN or has |x| <= 1 + 2^-21, so only the lower
+// end of rcp_nr's range needs a check; a NaN fails it), and whether the reciprocal is finite (on the
+// fast path by construction: |1 / x| <= 2^95)
+__device__ __forceinline__ void recip3_unit(f3 d, f3& inv, bool& fin) {
+  if (__all(fabsf(d.x) >= 0x1p-95f && fabsf(d.y) >= 0x1p-95f && fabsf(d.z) >= 0x1p-95f)) {
+    inv = mk(rcp_nr(d.x), rcp_nr(d.y), rcp_nr(d.z));
+    fin = true;
+  } else {
+    inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    fin = __builtin_isfinite(inv.x) && __builtin_isfinite(inv.y) && __builtin_isfinite(inv.z);
+  }
+}
 __device__ __forceinline__ f3 xyz(float4 v) { return mk(v.x, v.y, v.z); }
 // floor(n / d) for n < 2^31 by the host's multiplier (rt2_layout.h Magic): v_mad_u64_u32 + shift
 __device__ __forceinline__ uint32_t udiv(uint32_t n, Magic d) { return (uint32_t)(((uint64_t)n * d.m) >> d.s); }
@@ -673,7 +685,9 @@ __device__ __forceinline__ f3 rand_unit_vec3(G& g) {
   float u[2];
   g.template take<2>(u);
   const float z = 1.0f - 2.0f * u[0];
-  const float r = sqrtf(1.0f - z * z);
+  // 1 - z^2 is 0 or >= 2^-22 for every 24-bit uniform, where sqrt_nr is the IEEE square root
+  // (rt2_selftest which 9 checks all 2^24 inputs)
+  const float r = sqrt_nr(1.0f - z * z);
   float c, s;
   cos_sin_2pi(u[1], c, s);
   return mk(r * c, r * s, z);
@@ -826,7 +840,33 @@ __device__ __forceinline__ bool quad_t(const Nodes<kMode>& N, uint32_t off, f3 o
   return true;
 }
 
-// Sphere::Hit (Sphere.cpp:7-37): exclusive interval (Surrounds); uv is dead output
+// The range in which a sphere root (hh -+ sq) / a may be taken as div_by_inv(num, a, fl(1/a)): every
+// intermediate normal and finite. 2^-60 <= a <= 2^60 and |hh| + sq <= 2^60 bound the quotient and the
+// products; each numerator is +0 (exact: 0 * inv = +0 = +0 / a) or has |num| >= max(2^-70, 2^-60 a),
+// so the quotient is >= 2^-60 and the fma residual (about 2^-24 |num|) stays above 2^-126. A cancelled
+// numerator below that (a medium's boundary queries accept every root, ConstantMedium.cpp:18) or -0
+// (IEEE gives -0 / a = -0, the correction +0) takes the IEEE division. rt2_selftest which 8 checks the
+// fast roots against IEEE division on rays from near a sphere's surface (cancelled numerators down to
+// the subnormal range) at every interval kind.
+__device__ __forceinline__ bool sphere_fast_ok(float a, float hh, float sq) {
+  const float n1 = hh - sq, n2 = hh + sq;
+  const float lo = fmaxf(0x1p-70f, 0x1p-60f * a);
+  const bool ok1 = fabsf(n1) >= lo || __float_as_uint(n1) == 0u;
+  const bool ok2 = fabsf(n2) >= lo || __float_as_uint(n2) == 0u;
+  return a >= 0x1p-60f && a <= 0x1p60f && fabsf(hh) + sq <= 0x1p60f && ok1 && ok2;
+}
+// The same for a query on [tmin, tmax] with tmin >= 0.001 (every query but a medium's boundary
+// queries): an accepted root then has |num| >= 0.001 a >= 2^-70 (the residual stays normal), and a
+// root whose numerator is below that range, computed to within a few ulps, is far below tmin on either
+// path, so it is rejected either way; only a and the products' range need the check.
+__device__ __forceinline__ bool sphere_fast_ok_pos(float a, float hh, float sq) {
+  return a >= 0x1p-60f && a <= 0x1p60f && fabsf(hh) + sq <= 0x1p60f;
+}
+// Sphere::Hit (Sphere.cpp:7-37): exclusive interval (Surrounds); uv is dead output. kDiv 0: the fast
+// roots when every lane of the wave is in sphere_fast_ok_pos's range (queries with tmin >= 0.001);
+// 4: in sphere_fast_ok's (any interval: a medium's boundary queries); 1 / 3: when this lane is in
+// sphere_fast_ok's / sphere_fast_ok_pos's range (selftest); 2: IEEE division only (selftest reference).
+template <int kDiv = 0>
 __device__ __forceinline__ bool sphere_t_rec(float4 r0, float4 r1, f3 o, f3 d, float time, float tmin, float tmax,
                                              float& t_out) {
   f3 center = xyz(r0) + xyz(r1) * time;
@@ -838,10 +878,13 @@ __device__ __forceinline__ bool sphere_t_rec(float4 r0, float4 r1, f3 o, f3 d, f
   if (disc < 0.0f) return false;
   float sq = sqrtf(disc);
   // The two roots (hh -+ sq) / a: by the correctly rounded 1/a with one fma correction
-  // (div_by_inv, equal to IEEE division for every pair of significands) when the wave's a and
-  // numerators keep its intermediates normal and finite (an accepted root >= tmin then has
-  // |num| >= 0.001 a >= 2^-70, so its correction term stays above 2^-126); IEEE division otherwise.
-  const bool fast = __all(a >= 0x1p-60f && a <= 0x1p60f && fabsf(hh) + sq <= 0x1p60f);
+  // (div_by_inv, equal to IEEE division for every pair of significands) in sphere_fast_ok's range;
+  // IEEE division otherwise.
+  bool fast = false;
+  if constexpr (kDiv == 0) fast = __all(sphere_fast_ok_pos(a, hh, sq));
+  if constexpr (kDiv == 4) fast = __all(sphere_fast_ok(a, hh, sq));
+  if constexpr (kDiv == 1) fast = sphere_fast_ok(a, hh, sq);
+  if constexpr (kDiv == 3) fast = sphere_fast_ok_pos(a, hh, sq);
   const float inv_a = fast ? rcp_nr(a) : 0.0f;
   float root = fast ? div_by_inv(hh - sq, a, inv_a) : (hh - sq) / a;
   if (!(tmin < root && root < tmax)) {
@@ -851,10 +894,10 @@ __device__ __forceinline__ bool sphere_t_rec(float4 r0, float4 r1, f3 o, f3 d, f
   t_out = root;
   return true;
 }
-template <int kMode>
+template <int kMode, int kDiv = 0>
 __device__ __forceinline__ bool sphere_t(const Nodes<kMode>& N, uint32_t off, f3 o, f3 d, float time, float tmin,
                                          float tmax, float& t_out) {
-  return sphere_t_rec(N[off], N[off + 1], o, d, time, tmin, tmax, t_out);
+  return sphere_t_rec<kDiv>(N[off], N[off + 1], o, d, time, tmin, tmax, t_out);
 }
 
 // Quad::Hit split in two: the candidate (pure function of the ray) and the interval test. The
@@ -978,14 +1021,15 @@ __device__ __forceinline__ bool quad_cand_u(uint32_t axis, const float* w, f3 o,
   }
 }
 
-template <uint32_t F, int kMode>
+// (kBoundary: a medium's boundary query, on any interval)
+template <uint32_t F, int kMode, bool kBoundary = false>
 __device__ __forceinline__ bool prim_t(const Nodes<kMode>& N, uint32_t ref, f3 o, f3 d, float time, float tmin,
                                        float tmax, float& t, Counters& cnt) {
   uint32_t off = ref & kOffsetMask;
   if constexpr (Has<F, kFeatSphere>()) {
     if ((ref >> 28) == kSphere) {
       cnt.sphere++;
-      return sphere_t(N, off, o, d, time, tmin, tmax, t);
+      return sphere_t<kMode, kBoundary ? 4 : 0>(N, off, o, d, time, tmin, tmax, t);
     }
   }
   cnt.quad++;
@@ -996,13 +1040,13 @@ __device__ __forceinline__ bool prim_t(const Nodes<kMode>& N, uint32_t ref, f3 o
 template <uint32_t F, int kMode>
 __device__ __forceinline__ bool boundary_t(const Nodes<kMode>& N, uint32_t ref, f3 o, f3 d, float time, float lo,
                                            float hi, float& t_out, Counters& cnt) {
-  if ((ref >> 28) != kList) return prim_t<F>(N, ref, o, d, time, lo, hi, t_out, cnt);
+  if ((ref >> 28) != kList) return prim_t<F, kMode, true>(N, ref, o, d, time, lo, hi, t_out, cnt);
   uint32_t off = ref & kOffsetMask;
   uint32_t n = N.word(off, 0);
   bool any = false;
   for (uint32_t k = 0; k < n; k++) {
     float t;
-    if (prim_t<F>(N, N.word(off + 1, k), o, d, time, lo, hi, t, cnt)) {
+    if (prim_t<F, kMode, true>(N, N.word(off + 1, k), o, d, time, lo, hi, t, cnt)) {
       any = true;
       hi = t;
     }
@@ -1072,7 +1116,8 @@ __device__ __forceinline__ bool boundary_prim_lin(const void* recs, uint32_t ref
   const uint32_t off = ref & kOffsetMask;
   if (Has<F, kFeatSphere>() && (ref >> 28) == kSphere) {
     cnt.sphere++;
-    return sphere_t(Nodes<kModeLinear>{reinterpret_cast<const float4*>(recs), 0u}, off, o, d, time, lo, hi, t_out);
+    return sphere_t<kModeLinear, 4>(Nodes<kModeLinear>{reinterpret_cast<const float4*>(recs), 0u}, off, o, d, time, lo,
+                                    hi, t_out);
   }
   cnt.quad++;
   u32x16 a;
@@ -1505,6 +1550,9 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
       // order (issue-bound: one candidate at a time beats two interleaved, measured)
       const uint32_t run = st.w;
       uint32_t codes = st.y;
+      // the run's interval test in_interval(t, tmin, tmax) as key(t) <= kmax with key(x) = bits(x) -
+      // bits(tmin) (kmax = key(tmax), updated with the accepted t's key; tmax = its float after the run)
+      uint32_t kmax = bits(tmax) - bits(tmin);
       for (uint32_t k = 0; k < run; k++, codes >>= 3) {
         const uint32_t o0 = off + 5u * k;
         const uint32_t c0 = codes & 7u;
@@ -1548,11 +1596,13 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
           asm volatile("" ::"v"(t2), "v"((int)ok2));
         }
 #endif
-        if (ok0 & in_interval(t0, tmin, tmax)) {
-          tmax = t0;
+        const uint32_t kt = bits(t0) - bits(tmin);
+        if (ok0 & (kt <= kmax)) {
+          kmax = kt;
           prim = make_ref(kind0, o0);
         }
       }
+      tmax = uf(kmax + bits(tmin));
       next = at + run;
     } else if (Has<F, kFeatSphere>() && kind == kSphere) {
       float t;
@@ -1569,15 +1619,23 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
     } else if (Has<F, kFeatXform>() && kind == kXform) {
       if (kStats) cnt.xform++;
       const u32x16 m = sld16(recs, off * 16u);  // inverse-model columns
-      f3 no = mk((uf(m[0]) * o.x + uf(m[4]) * o.y) + (uf(m[8]) * o.z + uf(m[12])),
-                 (uf(m[1]) * o.x + uf(m[5]) * o.y) + (uf(m[9]) * o.z + uf(m[13])),
-                 (uf(m[2]) * o.x + uf(m[6]) * o.y) + (uf(m[10]) * o.z + uf(m[14])));
-      f3 nd = mk(uf(m[0]) * d.x + uf(m[4]) * d.y + uf(m[8]) * d.z, uf(m[1]) * d.x + uf(m[5]) * d.y + uf(m[9]) * d.z,
-                 uf(m[2]) * d.x + uf(m[6]) * d.y + uf(m[10]) * d.z);
+      f3 no, nd;
+      if (m[11] == kXformYAxis) {
+        // a transform about y (compile.cpp YAxisPattern): the products of the +-0 entries col0.y,
+        // col1.x, col1.z, col2.y are left out of the sums below (DESIGN.md §4 "Transforms about y")
+        no = mk(uf(m[0]) * o.x + (uf(m[8]) * o.z + uf(m[12])), uf(m[5]) * o.y + uf(m[13]),
+                uf(m[2]) * o.x + (uf(m[10]) * o.z + uf(m[14])));
+        nd = mk(uf(m[0]) * d.x + uf(m[8]) * d.z, uf(m[5]) * d.y, uf(m[2]) * d.x + uf(m[10]) * d.z);
+      } else {
+        no = mk((uf(m[0]) * o.x + uf(m[4]) * o.y) + (uf(m[8]) * o.z + uf(m[12])),
+                (uf(m[1]) * o.x + uf(m[5]) * o.y) + (uf(m[9]) * o.z + uf(m[13])),
+                (uf(m[2]) * o.x + uf(m[6]) * o.y) + (uf(m[10]) * o.z + uf(m[14])));
+        nd = mk(uf(m[0]) * d.x + uf(m[4]) * d.y + uf(m[8]) * d.z, uf(m[1]) * d.x + uf(m[5]) * d.y + uf(m[9]) * d.z,
+                uf(m[2]) * d.x + uf(m[6]) * d.y + uf(m[10]) * d.z);
+      }
       o = no;
       d = normalize(nd);
-      inv = recip3(d);
-      fin = finite3(inv);
+      recip3_unit(d, inv, fin);
 #if RT2_EXP_TWICE & 2048
       {
         f3 o2 = o;
@@ -1763,8 +1821,13 @@ __device__ __forceinline__ void resolve_hit(const Nodes<kMode>& N, const HitRef&
     for (uint32_t x = h.xf; x != kRefNone;) {
       uint32_t xo = x & kOffsetMask;
       float4 m0 = N[xo + 4], m1 = N[xo + 5], m2 = N[xo + 6], m3 = N[xo + 7];
-      p = mk((m0.x * p.x + m1.x * p.y) + (m2.x * p.z + m3.x), (m0.y * p.x + m1.y * p.y) + (m2.y * p.z + m3.y),
-             (m0.z * p.x + m1.z * p.y) + (m2.z * p.z + m3.z));
+      // (c2.w: the transform's pattern in the threaded program's copy, 0 in the node array)
+      if (kMode == kModeLinear && N.word(xo + 2, 3) == kXformYAxis) {  // M's +-0 products left out
+        p = mk(m0.x * p.x + (m2.x * p.z + m3.x), m1.y * p.y + m3.y, m0.z * p.x + (m2.z * p.z + m3.z));
+      } else {
+        p = mk((m0.x * p.x + m1.x * p.y) + (m2.x * p.z + m3.x), (m0.y * p.x + m1.y * p.y) + (m2.y * p.z + m3.y),
+               (m0.z * p.x + m1.z * p.y) + (m2.z * p.z + m3.z));
+      }
       // (a medium's hit normal is never read: Isotropic::Scatter ignores it, Material.cpp:76-83)
       const float4 c1 = N[xo + 1];
       if (!(Has<F, kFeatMedium>() && kind == kMedium) && !wnormal) {
@@ -1875,7 +1938,7 @@ __device__ __forceinline__ void camera_ray(const RenderParams& P, G& g, uint32_t
       // RandInUnitDisk (uniform in the unit disk) by the inverse-CDF map r = sqrt(u), phi = 2 pi v
       float w[2];
       g.template take<2>(w);
-      const float rr = sqrtf(w[0]);
+      const float rr = sqrt_nr(w[0]);  // (every 24-bit uniform: rt2_selftest which 9)
       float cd, sd;
       cos_sin_2pi(w[1], cd, sd);
       const float dx = rr * cd, dy = rr * sd;
@@ -2530,6 +2593,9 @@ KernelFn Kernel(int v, int mode, bool stats) {
 //   which 4: acc_slab (accelerated-list padded slab) never culls a box the exact padded slab accepts
 //   which 5: rcp_nr == 1/x for every float in its range (exhaustive over the 2^32 bit patterns)
 //   which 6: div_by_inv's single correction == a / b for every pair of significands (n = 2^46)
+//   which 7: the same for every numerator significand against n / 2^23 divisor significands each
+//   which 8: sphere_t_rec's fast roots (sphere_fast_ok) == IEEE division, cancelled numerators included
+//   which 9: sqrt_nr == sqrt at the samplers' inputs for every 24-bit uniform (n = 2^24)
 __device__ __forceinline__ float rand_float(uint32_t bits, int emin, int emax, uint32_t sel) {
   const int e = emin + (int)(sel % (uint32_t)(emax - emin + 1));
   return __uint_as_float((bits & 0x807FFFFFu) | ((uint32_t)(e + 127) << 23));
@@ -2543,6 +2609,30 @@ __global__ void selftest_kernel(int which, unsigned long long n, uint32_t seed, 
       // algorithm and the quotient scale exactly with the exponents)
       const float a = __uint_as_float(0x3F800000u | (uint32_t)(idx >> 23));
       const float b = __uint_as_float(0x3F800000u | ((uint32_t)idx & 0x7FFFFFu));
+      checked++;
+      if (__float_as_uint(div_by_inv(a, b, rcp_nr(b))) != __float_as_uint(a / b)) bad++;
+      continue;
+    }
+    if (which == 9) {
+      // every 24-bit uniform u (n = 2^24): sqrt_nr against IEEE sqrt at the samplers' two inputs,
+      // 1 - z^2 with z = 1 - 2u (rand_unit_vec3) and u itself (the defocus disk's radius)
+      if (idx >= (1ull << 24)) continue;
+      const float u = to_unit((uint32_t)idx << 8);
+      const float z = 1.0f - 2.0f * u, x = 1.0f - z * z;
+      checked++;
+      if (__float_as_uint(sqrt_nr(x)) != __float_as_uint(sqrtf(x)) ||
+          __float_as_uint(sqrt_nr(u)) != __float_as_uint(sqrtf(u)))
+        bad++;
+      continue;
+    }
+    if (which == 7) {
+      // every numerator significand (2^23 values of a in [1, 2)), each against n / 2^23 divisor
+      // significands: b = 1, b = 2 - 2^-23 and a scrambled stride over the rest (neighbouring a values
+      // see different divisors)
+      const uint32_t sa = (uint32_t)idx & 0x7FFFFFu, j = (uint32_t)(idx >> 23);
+      uint32_t sb = (sa * 0x9E3779B1u + j * 0x85EBCA77u) ^ (j * 0x2545F491u) ^ (sa >> 7);
+      sb = j == 0u ? 0u : (j == 1u ? 0x7FFFFFu : sb & 0x7FFFFFu);
+      const float a = __uint_as_float(0x3F800000u | sa), b = __uint_as_float(0x3F800000u | sb);
       checked++;
       if (__float_as_uint(div_by_inv(a, b, rcp_nr(b))) != __float_as_uint(a / b)) bad++;
       continue;
@@ -2612,6 +2702,58 @@ __global__ void selftest_kernel(int which, unsigned long long n, uint32_t seed, 
       ref = ref && t0 * (1.0 + 1e-6) < t1 * (1.0 - 1e-6);
       checked++;
       if (ref && !got) bad++;
+    } else if (which == 8) {
+      // sphere roots: sphere_t_rec with the fast roots wherever this lane is in sphere_fast_ok's range
+      // against IEEE division, on rays from on / near a sphere's surface (c about 0: one root's
+      // numerator hh -+ sq cancels, down to the subnormal range) and generic rays, spheres at scales
+      // 2^-50 .. 2^20, every interval kind of the kernel (Surrounds on [0.001, t], the medium's boundary
+      // queries on [-FLT_MAX, FLT_MAX] and [fl(t1 + 1e-4), FLT_MAX], tiny bounds around 0). Every lane
+      // is compared; `checked` counts the admitted lanes whose smaller numerator cancelled (|num| <
+      // 2^-20 |hh|, or 0).
+      uint32_t s0, s1, s2, s3;
+      philox(seed, 0x5F3Eu, (uint32_t)idx, (uint32_t)(idx >> 32), 1u, s0, s1, s2, s3);
+      const float S = __uint_as_float((uint32_t)(127 - 50 + (int)(r0 % 71u)) << 23);  // 2^-50 .. 2^20
+      const float rad = S * (0.25f + to_unit(r1));
+      const f3 cen = mk(S * (4.0f * to_unit(r2) - 2.0f), S * (4.0f * to_unit(r3) - 2.0f), S * (4.0f * to_unit(s0) - 2.0f));
+      const f3 u = normalize(mk(2.0f * to_unit(s1) - 1.0f, 2.0f * to_unit(s2) - 1.0f, 2.0f * to_unit(s3) + 0.01f - 1.0f));
+      const uint32_t kind = r0 >> 29;
+      f3 o;
+      if (kind <= 2u) {  // on the surface (rounded), a few ulps off it, or about a sphere at the origin
+        const f3 c2 = kind == 2u ? mk(0.0f, 0.0f, 0.0f) : cen;
+        o = c2 + u * rad;
+        if (kind == 1u) o = o * (1.0f + (float)((int)(s0 & 7u) - 4) * 0x1p-23f);
+      } else {
+        o = cen + mk(S * (8.0f * to_unit(r3 ^ s1) - 4.0f), S * (8.0f * to_unit(r2 ^ s2) - 4.0f), S * (8.0f * to_unit(r1 ^ s3) - 4.0f));
+      }
+      const f3 cen_s = kind == 2u ? mk(0.0f, 0.0f, 0.0f) : cen;
+      // direction: random, or nearly tangent to the sphere at o (hh about 0), scaled 2^-20 .. 2^20
+      f3 v = mk(2.0f * to_unit(s2 ^ r1) - 1.0f, 2.0f * to_unit(s3 ^ r2) - 1.0f, 2.0f * to_unit(s1 ^ r3) - 1.0f);
+      if ((s1 & 3u) == 0u) v = v - u * dot(v, u);
+      const float ds = __uint_as_float((uint32_t)(127 - 20 + (int)(s0 % 41u)) << 23);
+      const f3 d = v * ds;
+      const uint32_t ik = s2 & 3u;
+      const float tmin = ik == 0u ? -FLT_MAX
+                       : ik == 1u ? 0.001f
+                       : ik == 2u ? ((s3 & 1u) ? -1.0f : 1.0f) * __uint_as_float((uint32_t)(127 - (int)(s3 % 126u)) << 23)
+                                  : (float)((double)(S * (2.0f * to_unit(s0 ^ s3) - 1.0f)) + 0.0001);
+      const float tmax = (s3 & 8u) ? FLT_MAX : fabsf(S) * 4.0f * (to_unit(r2 ^ s0) + 0.01f);
+      const float4 q0 = make_float4(cen_s.x, cen_s.y, cen_s.z, rad), q1 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      float tf = 0.0f, ti = 0.0f;
+      const bool hf = sphere_t_rec<1>(q0, q1, o, d, 0.0f, tmin, tmax, tf);
+      const bool hi = sphere_t_rec<2>(q0, q1, o, d, 0.0f, tmin, tmax, ti);
+      if (hf != hi || (hf && __float_as_uint(tf) != __float_as_uint(ti))) bad++;
+      // the regular queries' guard (sphere_fast_ok_pos) on [0.001, tmax]
+      float tp = 0.0f, tq = 0.0f;
+      const bool hp = sphere_t_rec<3>(q0, q1, o, d, 0.0f, 0.001f, tmax, tp);
+      const bool hq = sphere_t_rec<2>(q0, q1, o, d, 0.0f, 0.001f, tmax, tq);
+      if (hp != hq || (hp && __float_as_uint(tp) != __float_as_uint(tq))) bad++;
+      // (the operations of sphere_t_rec up to its guard)
+      const f3 oc = cen_s - o;
+      const float a = dot(d, d), hh = dot(d, oc), c = dot(oc, oc) - rad * rad, disc = hh * hh - a * c;
+      if (disc >= 0.0f) {
+        const float sq = sqrtf(disc), nmin = fminf(fabsf(hh - sq), fabsf(hh + sq));
+        if (sphere_fast_ok(a, hh, sq) && (nmin < 0x1p-20f * fabsf(hh) || nmin == 0.0f)) checked++;
+      }
     } else if (which == 5) {
       // every float bit pattern (n = 2^32): rcp_nr against IEEE 1/x over its whole range
       const float x = __uint_as_float((uint32_t)idx);

@@ -79,7 +79,10 @@ inline constexpr uint32_t make_ref(uint32_t kind, uint32_t off) { return (kind <
 //  LIST  : (count bits, flags bits, 0, 0) then child refs, 4 per record. flags bit0 = every
 //          child is a QUAD or SPHERE (iterated inline, no stack traffic).
 //  XFORM : (invM col0.xyz, child_ref bits) (invM col1.xyz, parent_xform_ref bits)
-//          (invM col2.xyz, 0) (invM col3.xyz, 0) (M col0.xyz,0) (M col1.xyz,0) (M col2.xyz,0) (M col3.xyz,0)
+//          (invM col2.xyz, pattern bits) (invM col3.xyz, 0) (M col0.xyz,0) (M col1.xyz,0) (M col2.xyz,0)
+//          (M col3.xyz,0); pattern (threaded-program copies only, else 0): kXformYAxis when col0.y,
+//          col1.x, col1.z and col2.y of both matrices are +-0 (a transform about y, compile.cpp
+//          YAxisPattern): the kernel leaves their +-0 products out
 //  MEDIUM: (neg_inv_density, material bits, boundary_ref bits, 0)
 //          In the threaded program's record copy, a boundary that is a list of at most
 //          kBoundaryAAMax unit-normal axis-aligned quads (a box in the medium's space) also has its
@@ -99,6 +102,7 @@ inline constexpr uint32_t make_ref(uint32_t kind, uint32_t off) { return (kind <
 //          centroids along the node's split axis (kind - kAccBvh); children are ACCBVH or
 //          ACCSPHERE refs (an ACCSPHERE ref points at the child's SPHERE record)
 constexpr uint32_t kListLeafOnly = 1u;
+constexpr uint32_t kXformYAxis = 1u;
 // The reciprocal direction component an accelerated list's padded slab test uses (render.hip lane
 // walk: ax = fma(lo - o, inv, -pad inv), bx = fma(hi - o, inv, pad inv)): inv itself when finite,
 // else +-2^100. With inv = +-inf (d = +-0) the fma form gives NaN or -inf for an origin inside the

@@ -1,0 +1,10 @@
+#!/bin/bash
+# Round 5: the GPU parity suite (incl. the new selftests) on the current build, then an A/B of
+# library variants (raytrace2_amd/lib/ablate) on C2 / C3 / C4 / C5 bench shapes.
+set -u
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 200 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
+rc=$?
+echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
+if [ $rc -ne 0 ]; then exit $rc; fi
+VARIANTS="${VARIANTS:-noguard guard yaxis}" REPS=${REPS:-2} CONFIGS="|;|--scene cornell_box_volume.json --spp 1000;|--scene final_render_book_1.json --width 1920 --height 1080 --spp 100;|--scene book2_final_scene_10000_samples.json --width 800 --height 800 --spp 1000" AB_NAME=ab_r05b bash tools/gpu_ab.sh
