@@ -117,7 +117,10 @@ RT2_API int rt2_tracer_set_launch_frames(rt2_tracer* tr, int frames_per_launch);
  * ones at the end of the launch. 0 = one chunk (each pixel's frames in one item). Every frame's
  * sample goes to a per-frame buffer and is summed in frame order after the launch, so results do
  * not depend on the split. The buffer is bounded by `bytes` (default 16 GiB): a render needing
- * more runs as several launches. */
+ * more runs as several launches. The bound applies to each of the tracer's two launch slots
+ * (consecutive launches alternate between two sample buffers so that a launch's tail overlaps the
+ * next launch): the device memory the samples may take is 2 x `bytes` (32 GiB by default, of the
+ * MI355X's 288 GB), per GPU. */
 RT2_API int rt2_tracer_set_lazy_frames(rt2_tracer* tr, int max_queued);
 RT2_API int rt2_tracer_flush(rt2_tracer* tr); /* launch the queued frames now (does not wait) */
 RT2_API int rt2_tracer_set_work_split(rt2_tracer* tr, int items_per_lane);

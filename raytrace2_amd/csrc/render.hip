@@ -1640,14 +1640,23 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
       {
         f3 o2 = o;
         asm volatile("" : "+v"(o2.x), "+v"(o2.y), "+v"(o2.z));
-        const f3 n2 = mk((uf(m[0]) * o2.x + uf(m[4]) * o2.y) + (uf(m[8]) * o2.z + uf(m[12])),
-                         (uf(m[1]) * o2.x + uf(m[5]) * o2.y) + (uf(m[9]) * o2.z + uf(m[13])),
-                         (uf(m[2]) * o2.x + uf(m[6]) * o2.y) + (uf(m[10]) * o2.z + uf(m[14])));
-        const f3 d2 = normalize(mk(uf(m[0]) * o2.x + uf(m[4]) * o2.y + uf(m[8]) * o2.z,
-                                   uf(m[1]) * o2.x + uf(m[5]) * o2.y + uf(m[9]) * o2.z,
-                                   uf(m[2]) * o2.x + uf(m[6]) * o2.y + uf(m[10]) * o2.z));
-        const f3 i2 = recip3(d2);
-        asm volatile("" ::"v"(n2.x), "v"(n2.y), "v"(n2.z), "v"(i2.x), "v"(i2.y), "v"(i2.z));
+        f3 n2, e2;
+        if (m[11] == kXformYAxis) {
+          n2 = mk(uf(m[0]) * o2.x + (uf(m[8]) * o2.z + uf(m[12])), uf(m[5]) * o2.y + uf(m[13]),
+                  uf(m[2]) * o2.x + (uf(m[10]) * o2.z + uf(m[14])));
+          e2 = mk(uf(m[0]) * o2.x + uf(m[8]) * o2.z, uf(m[5]) * o2.y, uf(m[2]) * o2.x + uf(m[10]) * o2.z);
+        } else {
+          n2 = mk((uf(m[0]) * o2.x + uf(m[4]) * o2.y) + (uf(m[8]) * o2.z + uf(m[12])),
+                  (uf(m[1]) * o2.x + uf(m[5]) * o2.y) + (uf(m[9]) * o2.z + uf(m[13])),
+                  (uf(m[2]) * o2.x + uf(m[6]) * o2.y) + (uf(m[10]) * o2.z + uf(m[14])));
+          e2 = mk(uf(m[0]) * o2.x + uf(m[4]) * o2.y + uf(m[8]) * o2.z, uf(m[1]) * o2.x + uf(m[5]) * o2.y + uf(m[9]) * o2.z,
+                  uf(m[2]) * o2.x + uf(m[6]) * o2.y + uf(m[10]) * o2.z);
+        }
+        const f3 d2 = normalize(e2);
+        f3 i2;
+        bool f2;
+        recip3_unit(d2, i2, f2);
+        asm volatile("" ::"v"(n2.x), "v"(n2.y), "v"(n2.z), "v"(i2.x), "v"(i2.y), "v"(i2.z), "v"((int)f2));
       }
 #endif
       cur_xf = make_ref(kXform, off);
