@@ -15,29 +15,89 @@ namespace rt2 {
 
 namespace {
 
-// The 8 test words (sD, w[K], q[A], q[B], u[A], u[B], v[A], v[B]) of a unit-normal axis-aligned
-// quad (QUAD record r, axis code K + 4, rt2_layout.h QUADAA) when it is a rectangle in the A-B plane
-// (one edge along A, the other along B, the off-axis components exactly zero), with the edge along A
-// first: a quad whose u runs along B is recorded as its mirror (u and v swapped, w negated), whose
-// Quad::Hit interior coordinates are (beta, alpha) of the original, bit for bit (a - b = -(b - a)
-// and negation commutes with rounding), so the [0, 1]^2 test decides the same. The kernel's
-// rectangle test then reads u[A] and v[B] only. False for other quads (kept on the general path).
+// Quad::Hit's interior decision on one coordinate of a rectangle, 0 <= c1 ((p - q) c2) <= 1 with the
+// float operations in that order (the rectangle forms below), as a function of the hit point's
+// coordinate p alone.
+bool CoordIn(float p, float q, float c1, float c2) {
+  const float a = c1 * ((p - q) * c2);
+  return 0.0f <= a && a <= 1.0f;
+}
+// Floats in the order of the reals as integers (-0 and +0 both 0) and back (0 -> +0).
+int64_t OrderKey(float f) {
+  uint32_t b;
+  memcpy(&b, &f, 4);
+  return (b & 0x80000000u) ? -(int64_t)(b & 0x7FFFFFFFu) : (int64_t)b;
+}
+float FromOrderKey(int64_t k) {
+  const uint32_t b = k >= 0 ? (uint32_t)k : ((uint32_t)(-k) | 0x80000000u);
+  float f;
+  memcpy(&f, &b, 4);
+  return f;
+}
+// The floats p with CoordIn(p, q, c1, c2) are one interval [lo, hi] of the reals' order, which holds
+// q: p -> p - q, y -> y c2 and y -> c1 y are each monotone under round-to-nearest (non-decreasing,
+// or non-increasing for a negative factor), so their composition g is monotone and {0 <= g <= 1} is
+// an interval; a p whose p - q overflows gives +-inf or NaN, rejected, and lies beyond both ends; a
+// zero's sign changes no decision (+-0 - q = -q; q = +-0 gives a +-0 product, accepted); g(q) = +-0.
+// Found by bisection over the order keys with the host's float arithmetic, which rounds as the device
+// does (SSE single precision, -ffp-contract=off). False when a word is not finite.
+bool CoordRange(float q, float c1, float c2, float& lo, float& hi) {
+  if (!std::isfinite(q) || !std::isfinite(c1) || !std::isfinite(c2) || !CoordIn(q, q, c1, c2)) return false;
+  const int64_t k0 = OrderKey(q), kinf = 0x7F800000;  // CoordIn(+-inf) is false
+  int64_t in = k0, out = kinf;
+  while (out - in > 1) {
+    const int64_t mid = in + (out - in) / 2;
+    (CoordIn(FromOrderKey(mid), q, c1, c2) ? in : out) = mid;
+  }
+  hi = FromOrderKey(in);
+  in = k0;
+  out = -kinf;
+  while (in - out > 1) {
+    const int64_t mid = in - (in - out) / 2;
+    (CoordIn(FromOrderKey(mid), q, c1, c2) ? in : out) = mid;
+  }
+  lo = FromOrderKey(in);
+  return true;
+}
+
+// The 8 test words (sD, lo[A], hi[A], lo[B], hi[B], 0, 0, 0) of a unit-normal axis-aligned quad
+// (QUAD record r, axis code K + 4, rt2_layout.h QUADAA) when it is a rectangle in the A-B plane (one
+// edge along A, the other along B, the off-axis components exactly zero). Its Quad::Hit interior
+// coordinates are alpha = w[K] ((p[A] - q[A]) v[B]) and beta = w[K] ((p[B] - q[B]) u[A]) (the cross
+// products' other terms are signed zeros, which decide nothing); a quad whose u runs along B is taken
+// as its mirror (u and v swapped, w negated), whose coordinates are (beta, alpha) of the original, bit
+// for bit (a - b = -(b - a), negation commutes with rounding). Each coordinate's [0, 1] test is then
+// lo <= p <= hi on the hit point's own coordinate (CoordRange): the kernel compares p[A] and p[B]
+// with the four bounds instead of computing alpha and beta. False for other quads, or when a word is
+// not finite (kept on the general path).
 bool RectAAWords(const float* r, int k, float out[8]) {
   const int a = (k + 1) % 3, b = (k + 2) % 3;
   const float* u = r + 8;
   const float* v = r + 12;
   const float wk = r[16 + k];
+  float c1, ca, cb;  // alpha = c1 ((p[A] - q[A]) ca), beta = c1 ((p[B] - q[B]) cb)
   if (u[b] == 0.0f && v[a] == 0.0f) {
-    const float rec[8] = {r[19], wk, r[4 + a], r[4 + b], u[a], u[b], v[a], v[b]};
-    std::copy(rec, rec + 8, out);
-    return true;
+    c1 = wk;
+    ca = v[b];
+    cb = u[a];
+  } else if (u[a] == 0.0f && v[b] == 0.0f) {
+    c1 = -wk;
+    ca = u[b];
+    cb = v[a];
+  } else {
+    return false;
   }
-  if (u[a] == 0.0f && v[b] == 0.0f) {
-    const float rec[8] = {r[19], -wk, r[4 + a], r[4 + b], v[a], v[b], u[a], u[b]};
-    std::copy(rec, rec + 8, out);
-    return true;
-  }
-  return false;
+  // The reduction to one product per coordinate leaves out the cross products' off-axis terms, e.g.
+  // w[A] (p[K] - q[K]) v[B]: +-0 while (p[K] - q[K]) v[B] is finite. p[K] is the hit point's coordinate
+  // along the normal, off the plane by rounding only (a few ulps of the ray origin's and q's
+  // coordinate); corners and edges within +-2^40 keep that product finite for every ray origin within
+  // +-2^80, far beyond any scene the loader accepts. Larger quads take the general path.
+  for (int i = 0; i < 3; i++)
+    if (!(std::fabs(r[4 + i]) <= 0x1p40f) || !(std::fabs(u[i]) <= 0x1p40f) || !(std::fabs(v[i]) <= 0x1p40f)) return false;
+  float rec[8] = {r[19], 0, 0, 0, 0, 0, 0, 0};
+  if (!CoordRange(r[4 + a], c1, ca, rec[1], rec[2]) || !CoordRange(r[4 + b], c1, cb, rec[3], rec[4])) return false;
+  std::copy(rec, rec + 8, out);
+  return true;
 }
 
 // The world-space normal of a quad under transforms, n_world = normalize(invM^T n) through the chain
@@ -676,6 +736,8 @@ void PackTextures(const Scene& s, CompiledScene& out) {
 }
 
 }  // namespace
+
+bool QuadAATestWords(const float* r, int k, float out[8]) { return RectAAWords(r, k, out); }
 
 bool CompileScene(const Scene& s, CompiledScene& out, std::string& err, bool accelerate_lists) {
   return CompileSceneWith(s, out, err, accelerate_lists, kAccDepthSlack);

@@ -969,38 +969,29 @@ __device__ __forceinline__ bool quad_cand_unit(const float* w, f3 o, f3 d, f3 in
   t_out = t;
   return !(fabsf(dk) <= 1e-8f) && (0.0f <= alpha && alpha <= 1.0f) && (0.0f <= beta && beta <= 1.0f);
 }
-// Range tests as unsigned compares of the float bits (each is one comparison mask instead of two
-// and a scalar AND: the lockstep kernels are bound by the scalar unit). Exact for every input:
-// 0 <= a <= 1 and 0 <= b <= 1 (IEEE compares) <=> max(bits(a + 0), bits(b + 0)) <= bits(1.0f):
-// x + 0 maps -0 to +0 and nothing else changes; any other negative value or a NaN has an image above
-// bits(1.0f).
-__device__ __forceinline__ bool unit_pair(float a, float b) {
-  return max(__float_as_uint(a + 0.0f), __float_as_uint(b + 0.0f)) <= 0x3F800000u;
-}
 // lo <= t <= hi (IEEE compares) for 0 < lo <= hi <= FLT_MAX <=> bits(t) - bits(lo) <= bits(hi) -
 // bits(lo) (unsigned, wrapping): positive floats order as their bits; a t below lo, a negative t,
 // -0, +inf or a NaN lands above the largest right side bits(FLT_MAX) - bits(lo).
 __device__ __forceinline__ bool in_interval(float t, float lo, float hi) {
   return __float_as_uint(t) - __float_as_uint(lo) <= __float_as_uint(hi) - __float_as_uint(lo);
 }
-// Unit-normal axis-aligned Quad::Hit from a QUADAA record r = (sD, w[K], q[A], q[B], u[A], u[B],
-// v[A], v[B]): the operations of quad_cand_unit on the same values. The compiler records only
-// rectangles, edge along A first (compile.cpp RectAAWords: u[B] = v[A] = 0 exactly), so the
-// cross products' second terms are signed zeros and alpha = w_K (pv_A v_B), beta = w_K (u_A pv_B)
-// decide the same (a non-finite pv_A or pv_B, which gave a NaN, now gives a non-finite alpha or
-// beta: rejected either way).
+// Unit-normal axis-aligned Quad::Hit from a QUADAA record r = (sD, lo[A], hi[A], lo[B], hi[B]): t as
+// quad_cand_unit computes it, the hit point's coordinates p[A], p[B] as Quad::Hit computes them
+// (r.at(t)), and the interior test alpha, beta in [0, 1] as lo <= p <= hi on each coordinate: the
+// compiler records rectangles only, whose alpha depends on p[A] alone through monotone rounded
+// operations and beta on p[B] alone, and the bounds are the first and last floats it accepts
+// (compile.cpp CoordRange), so the decision is the same for every p, NaN and +-inf rejected.
 template <int K>
 __device__ __forceinline__ bool quad_aa(const float* r, f3 o, f3 d, f3 inv, float& t_out) {
   constexpr int A = (K + 1) % 3, B = (K + 2) % 3;
   const float dk = comp<K>(d);
   const float t = div_by_inv(r[0] - comp<K>(o), dk, comp<K>(inv));
-  const float pva = (comp<A>(o) + comp<A>(d) * t) - r[2];
-  const float pvb = (comp<B>(o) + comp<B>(d) * t) - r[3];
-  const float alpha = r[1] * (pva * r[7]);  // w . cross(pv, v)
-  const float beta = r[1] * (r[4] * pvb);   // w . cross(u, pv)
+  const float pa = comp<A>(o) + comp<A>(d) * t;
+  const float pb = comp<B>(o) + comp<B>(d) * t;
   t_out = t;
-  // (bitwise: both coordinates are computed for every lane, no divergent branch)
-  return (int)!(fabsf(dk) <= 1e-8f) & (int)unit_pair(alpha, beta);
+  // (bitwise: both coordinates are tested for every lane, no divergent branch)
+  return (int)!(fabsf(dk) <= 1e-8f) & (int)(r[1] <= pa) & (int)(pa <= r[2]) & (int)(r[3] <= pb) &
+         (int)(pb <= r[4]);
 }
 __device__ __forceinline__ bool quad_aa_k(uint32_t k, const float* r, f3 o, f3 d, f3 inv, float& t) {
   if (k == 0u) return quad_aa<0>(r, o, d, inv, t);
@@ -1166,7 +1157,7 @@ __device__ __forceinline__ bool boundary_t_lin(const void* recs, uint32_t ref, f
 // A box boundary (rt2_layout.h MEDIUM, kBoundaryAAFlag): the closest of its quads on [lo, hi], list
 // order, each by the unit-normal test with IEEE division: t = (sD - o_K) / d_K is exactly
 // Quad::Hit's (D - n.o) / (n.d) for n = +-e_K (negation commutes with rounding), the interior test is
-// quad_cand_aa's, and the interval test is Contains (inclusive).
+// quad_aa's (the QUADAA bounds), and the interval test is Contains (inclusive).
 // (div_by_inv with the ray's reciprocal instead of the division: +0.7 % at 7 waves, -0.6 % at 8;
 // not used)
 template <int K>
@@ -1174,12 +1165,11 @@ __device__ __forceinline__ bool quad_aa_div(const uint32_t* r, f3 o, f3 d, float
   constexpr int A = (K + 1) % 3, B = (K + 2) % 3;
   const float dk = comp<K>(d);
   const float t = (uf(r[0]) - comp<K>(o)) / dk;
-  const float pva = (comp<A>(o) + comp<A>(d) * t) - uf(r[2]);
-  const float pvb = (comp<B>(o) + comp<B>(d) * t) - uf(r[3]);
-  const float alpha = uf(r[1]) * (pva * uf(r[7]));
-  const float beta = uf(r[1]) * (uf(r[4]) * pvb);
+  const float pa = comp<A>(o) + comp<A>(d) * t;
+  const float pb = comp<B>(o) + comp<B>(d) * t;
   t_out = t;
-  return (int)!(fabsf(dk) <= 1e-8f) & (int)unit_pair(alpha, beta);
+  return (int)!(fabsf(dk) <= 1e-8f) & (int)(uf(r[1]) <= pa) & (int)(pa <= uf(r[2])) & (int)(uf(r[3]) <= pb) &
+         (int)(pb <= uf(r[4]));
 }
 // Both boundary queries of ConstantMedium::Hit (ConstantMedium.cpp:14-58) on a box in one pass:
 // each quad's t and interior decision do not depend on the query's interval, so its quads are

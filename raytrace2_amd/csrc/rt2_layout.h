@@ -71,10 +71,11 @@ inline constexpr uint32_t make_ref(uint32_t kind, uint32_t off) { return (kind <
 //          In the threaded program's record copy (lind), v.w = the enclosing XFORM's lind ref.
 //  QUADAA: (threaded-program record copy of a quad with axis code K + 4 that is a rectangle in
 //          its plane; other unit-normal quads get code K + 1 in the program)
-//          (sD, w[K], q[A], q[B]) (u[A], u[B], v[A], v[B]) (n.xyz, D) (q.xyz, material bits)
-//          (axis bits, xform ref bits, 0, 0), A = (K + 1) % 3, B = (K + 2) % 3, with u[B] = v[A] = 0
-//          (a quad whose u runs along B is recorded mirrored: u, v swapped and w[K] negated,
-//          compile.cpp RectAAWords): the test reads the first 8 words only
+//          (sD, lo[A], hi[A], lo[B]) (hi[B], 0, 0, 0) (n.xyz, D) (q.xyz, material bits)
+//          (axis bits, xform ref bits, 0, 0), A = (K + 1) % 3, B = (K + 2) % 3: the hit point's
+//          in-plane coordinates p[A], p[B] that Quad::Hit's interior test accepts are exactly
+//          [lo[A], hi[A]] x [lo[B], hi[B]] (compile.cpp RectAAWords / CoordRange): the test reads
+//          the first 5 words only
 //  SPHERE: (c0.xyz, radius) (displacement.xyz, material bits)
 //  LIST  : (count bits, flags bits, 0, 0) then child refs, 4 per record. flags bit0 = every
 //          child is a QUAD or SPHERE (iterated inline, no stack traffic).

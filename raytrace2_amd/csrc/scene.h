@@ -158,6 +158,9 @@ bool CompileScene(const Scene& s, CompiledScene& out, std::string& err, bool acc
 constexpr int kAccDepthSlack = 2;
 bool CompileSceneWith(const Scene& s, CompiledScene& out, std::string& err, bool accelerate_lists,
                       int acc_depth_slack);
+// The 8 QUADAA test words of QUAD record r (20 floats, rt2_layout.h) with axis code k + 4, or false when
+// the quad takes the general path (compile.cpp RectAAWords; for tests/cpp/quadaa_bounds.cpp).
+bool QuadAATestWords(const float* r, int k, float out[8]);
 
 // Philox4x32-10 (shared constants with the kernel; see render.hip)
 void Philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1);

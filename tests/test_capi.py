@@ -79,3 +79,20 @@ def test_paired_program_steps_are_well_formed(tmp_path, scene, expect):
     r = subprocess.run([exe, os.path.join(ROOT, "scenes", scene + ".json"), str(expect)], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
     assert r.stdout.startswith("pairs=")
+
+
+def test_quadaa_bounds_decide_as_quad_hit(tmp_path):
+    """compile.cpp CoordRange (host only): the kernel's QUADAA interior test, lo <= p <= hi on the hit
+    point's two in-plane coordinates, decides as Quad::Hit's alpha/beta test (Quad.cpp:27-36) for
+    random rectangles of every orientation and hit points on, beside and far from the bounds, +-0,
+    +-inf and NaN (about 10 M decisions)."""
+    csrc = os.path.join(ROOT, "raytrace2_amd", "csrc")
+    exe = str(tmp_path / "quadaa_bounds")
+    r = subprocess.run(["g++", "-O1", "-std=c++17", "-ffp-contract=off", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
+                        "-I", csrc, "-o", exe, os.path.join(ROOT, "tests", "cpp", "quadaa_bounds.cpp")]
+                       + [os.path.join(csrc, f) for f in ("json.cpp", "scene.cpp", "compile.cpp")],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
+    r = subprocess.run([exe, "20000", "7"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr + r.stdout
+    assert r.stdout.startswith("rects=")

@@ -113,19 +113,21 @@ def test_book2_bench_kernel_spills_stay_out_of_the_trace(isa):
     assert scratch <= 96 and not deep, (scratch, deep[:5])
 
 
-def _loops(body):
-    """Every loop of a kernel body: (header label, depth, opcode counts of the loop's blocks)."""
+def _loops(body, lines=False):
+    """Every loop of a kernel body: (header label, depth, opcode counts of the loop's blocks), and with
+    lines=True the loop's instruction lines as a fourth element."""
     import collections
     blocks, cur = [], None
     for line in body.split("\n"):
         if line.startswith(".LBB") or line.startswith("; %bb"):
-            cur = [line.split()[0].rstrip(":") if line.startswith(".LBB") else line.split()[1], [line], []]
+            cur = [line.split()[0].rstrip(":") if line.startswith(".LBB") else line.split()[1], [line], [], []]
             blocks.append(cur)
         elif cur is not None and line.strip().startswith(";"):
             if not cur[2]:
                 cur[1].append(line)
         elif cur is not None and line.startswith("\t") and not line.strip().startswith("."):
             cur[2].append(line.split()[0])
+            cur[3].append(line.strip())
     out = []
     for b in blocks:
         m = re.search(r"Loop Header: Depth=(\d+)", " ".join(b[1]))
@@ -133,11 +135,13 @@ def _loops(body):
             continue
         h = b[0].lstrip(".L")
         c = collections.Counter()
+        ls = []
         for bb in blocks:
             txt = " ".join(bb[1])
             if bb is b or f"Header={h} " in txt or f"Parent Loop {h} " in txt or txt.endswith(f"Header={h}"):
                 c.update(bb[2])
-        out.append((b[0], int(m.group(1)), c))
+                ls.extend(bb[3])
+        out.append((b[0], int(m.group(1)), c, ls) if lines else (b[0], int(m.group(1)), c))
     return out
 
 
@@ -152,20 +156,23 @@ def test_cornell_quad_run_loop_keeps_the_scalar_issue_code_generation(isa):
     branches; -simplifycfg-sink-common=false keeps the three per-axis QUADAA bodies apart instead of one
     body fed by register copies). A toolchain that silently changed what they do would cost ~16 % with
     every other test green; this guard fails instead. The Cornell kernel's quad-run loop (the depth-3 loop
-    of the QUADAA test: the float-bit interior test's v_max_u32) must hold three separate interior tests
-    (one per axis), no exec-mask save per quad, and at most 36 SALU instructions (with the options: 30;
-    without them: 50 and one merged body); its trace loop at most 165 SALU (147; without: 190)."""
+    of the QUADAA test, whose interior test compares the hit point's two coordinates with four bounds
+    read from the record's scalar registers) must hold three separate interior tests (one per axis: 12
+    such compares), no exec-mask save per quad, and at most 46 SALU instructions (with the options: 39;
+    without them: 52 and one merged body, 4 such compares); its trace loop at most 165 SALU (144;
+    without: 180)."""
     _, body = _kernel(isa, "ILj4ELi2ELb0E")
-    loops = _loops(body)
-    quad = [(h, c) for h, d, c in loops if d == 3 and c["v_max_u32_e32"] + c["v_max_u32_e64"] > 0 and
-            any(k.startswith("s_load") for k in c)]
-    assert len(quad) == 1, [(h, d) for h, d, _ in loops]
-    _, c = quad[0]
-    umax = c["v_max_u32_e32"] + c["v_max_u32_e64"]
-    assert umax == 3, ("per-axis QUADAA bodies merged", umax)
+    loops = _loops(body, lines=True)
+    bound = re.compile(r"^v_cmp_(le|ge)_f32_e(32|64)\s+\S+,\s+s\d+,\s+v\d+$")
+    quad = [(h, c, ls) for h, d, c, ls in loops if d == 3 and any(k.startswith("s_load") for k in c) and
+            any(bound.match(x) for x in ls)]
+    assert len(quad) == 1, [(h, d) for h, d, _, _ in loops]
+    _, c, ls = quad[0]
+    ncmp = sum(1 for x in ls if bound.match(x))
+    assert ncmp == 12, ("per-axis QUADAA bodies merged", ncmp)
     assert c["s_and_saveexec_b64"] == 0, c["s_and_saveexec_b64"]
-    assert _salu(c) <= 36, _salu(c)
-    trace = [c for h, d, c in loops if d == 2 and _salu(c) > 60]
+    assert _salu(c) <= 46, _salu(c)
+    trace = [c for h, d, c, _ in loops if d == 2 and _salu(c) > 60]
     assert len(trace) == 1 and _salu(trace[0]) <= 165, [_salu(c) for c in trace]
 
 
