@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -858,6 +859,18 @@ int rt2_tracer_get_camera(const rt2_tracer* t, rt2_camera_desc* o) {
 namespace {
 constexpr uint32_t kFrameTileMinSteps = 256;  // threaded programs longer than this use frame tiles
 
+// Camera rays start within +-2^64 on every axis (center + the defocus disk's two half-axes): the
+// kernel's rectangle test (compile.cpp RectAAWords) is exact for ray origins within +-2^100, and a
+// scene the compiler gives that test lies within +-2^64 (Flattener::QuadAASpace).
+bool CameraOriginsBounded(const CameraParams& c) {
+  for (int k = 0; k < 3; k++)
+    if (!(std::fabs((double)c.center[k]) + std::fabs((double)c.defocus_u[k]) + std::fabs((double)c.defocus_v[k]) <=
+          0x1p64))
+      return false;
+  return true;
+}
+constexpr const char* kCameraRangeMsg = "camera origin or defocus disk outside +-2^64";
+
 Magic MakeMagic(uint32_t d) {  // rt2_layout.h Magic: floor(n / d) for n < 2^31
   uint32_t l = 0;
   while ((1ull << l) < (uint64_t)d) l++;
@@ -979,6 +992,7 @@ int LaunchFrames(rt2_tracer* t, int n_frames) {
   memcpy(p.background, t->background, sizeof(p.background));
   p.cam = t->camera.Params();  // RayTracer::Update → camera->Update() (RayTracer.cpp:56)
   if (p.cam.sqrt_spp <= 0) return Fail(RT2_ERR_INVALID, "samples_per_pixel gives sqrt_spp = 0");
+  if (!CameraOriginsBounded(p.cam)) return Fail(RT2_ERR_INVALID, kCameraRangeMsg);
   p.width = t->width;
   p.height = t->height;
   p.local_rows = t->local_rows;
@@ -1322,6 +1336,7 @@ int rt2_tracer_render(rt2_tracer* t, int n_frames) {
   if ((int64_t)t->frame_idx + t->queued + n_frames > 0x7FFFFFFF)
     return Fail(RT2_ERR_INVALID, "frame index overflow");
   if (t->camera.Params().sqrt_spp <= 0) return Fail(RT2_ERR_INVALID, "samples_per_pixel gives sqrt_spp = 0");
+  if (!CameraOriginsBounded(t->camera.Params())) return Fail(RT2_ERR_INVALID, kCameraRangeMsg);
   t->queued += n_frames;
   if (t->lazy_max > 0 && t->queued < t->lazy_max) return RT2_OK;
   return Flush(t);

@@ -57,6 +57,7 @@ bool CoordRange(float q, float c1, float c2, float& lo, float& hi) {
     (CoordIn(FromOrderKey(mid), q, c1, c2) ? in : out) = mid;
   }
   lo = FromOrderKey(in);
+  if (lo == 0.0f) lo = -0.0f;  // (the same bound; p - lo is then +0 for p = +-0, render.hip quad_aa)
   return true;
 }
 
@@ -89,9 +90,10 @@ bool RectAAWords(const float* r, int k, float out[8]) {
   }
   // The reduction to one product per coordinate leaves out the cross products' off-axis terms, e.g.
   // w[A] (p[K] - q[K]) v[B]: +-0 while (p[K] - q[K]) v[B] is finite. p[K] is the hit point's coordinate
-  // along the normal, off the plane by rounding only (a few ulps of the ray origin's and q's
-  // coordinate); corners and edges within +-2^40 keep that product finite for every ray origin within
-  // +-2^80, far beyond any scene the loader accepts. Larger quads take the general path.
+  // along the normal, off the plane by rounding only (|p[K] - q[K]| <= 2^-20 (|q[K]| + |o[K]|)), so
+  // corners and edges within +-2^40 keep that product finite for every ray origin o within +-2^100
+  // (the callers check it: Flattener::QuadAASpace, and the camera at every launch, capi.cpp).
+  // Larger quads take the general path.
   for (int i = 0; i < 3; i++)
     if (!(std::fabs(r[4 + i]) <= 0x1p40f) || !(std::fabs(u[i]) <= 0x1p40f) || !(std::fabs(v[i]) <= 0x1p40f)) return false;
   float rec[8] = {r[19], 0, 0, 0, 0, 0, 0, 0};
@@ -483,9 +485,10 @@ struct Flattener {
   // otherwise). Returns the medium record's word 3 (kBoundaryAAFlag | n << 24 | axis codes, 3 bits
   // per child), or 0 (general path only). The general copy of the boundary is kept for kernels
   // without the box path.
-  uint32_t BoundaryAA(int i, std::vector<float>& lind) {
+  uint32_t BoundaryAA(int i, uint32_t parent_xf, std::vector<float>& lind) {
     const Obj& o = s.objs[(size_t)i];
     if (o.kind != kList || o.children.empty() || o.children.size() > kBoundaryAAMax) return 0;
+    if (!QuadAASpace(parent_xf, lind)) return 0;
     uint32_t codes = 0;
     std::vector<float> words;
     for (size_t k = 0; k < o.children.size(); k++) {
@@ -523,6 +526,35 @@ struct Flattener {
     if ((octant >> (kind - kAccBvh)) & 1u) std::swap(near_ref, far_ref);
     if (!LinearizeAcc(near_ref, lin, lind, octant) || !LinearizeAcc(far_ref, lin, lind, octant)) return false;
     lin[4 * me + 1] = (uint32_t)(lin.size() / 4);
+    return true;
+  }
+  // Whether rays in the space of transform chain xf (innermost first) start within +-2^100, the bound
+  // RectAAWords' reduction needs: world-space origins (the camera, checked at every launch, and hit
+  // points on the geometry) lie within +-2^64 when the scene does, and each transform from the outermost
+  // in maps a bound B to |invM| B + |translation| (row sums of the inverse's 3x3 part, in double).
+  bool QuadAASpace(uint32_t xf, const std::vector<float>& lind) const {
+    const AABB& w = s.objs[(size_t)s.root].aabb;
+    const double lim = 0x1p64;
+    for (float v : {w.x.min, w.x.max, w.y.min, w.y.max, w.z.min, w.z.max})
+      if (!(std::fabs((double)v) <= lim)) return false;
+    std::vector<uint32_t> chain;
+    for (uint32_t x = xf; x != kRefNone;) {
+      chain.push_back(x & kOffsetMask);
+      uint32_t parent;
+      memcpy(&parent, &lind[4 * (size_t)(x & kOffsetMask) + 7], 4);
+      x = parent;
+    }
+    double b = lim;
+    for (size_t k = chain.size(); k-- > 0;) {
+      const float* m = &lind[4 * (size_t)chain[k]];  // invM columns c0..c3 (records 0-3, xyz)
+      double nb = 0;
+      for (int row = 0; row < 3; row++) {
+        const double r = std::fabs((double)m[row]) + std::fabs((double)m[4 + row]) + std::fabs((double)m[8 + row]);
+        nb = std::max(nb, r * b + std::fabs((double)m[12 + row]));
+      }
+      if (!(nb <= 0x1p100)) return false;
+      b = nb;
+    }
     return true;
   }
   // A transform about the y axis (every scene transform of the reference's files: ParseTransform's
@@ -618,7 +650,7 @@ struct Flattener {
       case kMedium: {
         if (ContainsAccList(o.child)) return false;  // boundary copies hold plain lists only
         uint32_t off = CopyRecords(src, kMediumRecords, lind);
-        lind[4 * off + 3] = Bits(BoundaryAA(o.child, lind));  // the box words follow the record
+        lind[4 * off + 3] = Bits(BoundaryAA(o.child, parent_xf, lind));  // the box words follow the record
         uint32_t b = CopyBoundary(o.child, lind);
         lind[4 * off + 2] = Bits(b);
         emit(kMedium, off, 0);
@@ -632,7 +664,7 @@ struct Flattener {
         float test[8];
         // a unit-normal quad that is not a rectangle in its plane takes the axis-aligned test
         // with division (code K + 1: the same decision and t)
-        if (axis >= 4 && axis <= 6 && !RectAAWords(r, (int)axis - 4, test)) axis -= 3;
+        if (axis >= 4 && axis <= 6 && !(QuadAASpace(parent_xf, lind) && RectAAWords(r, (int)axis - 4, test))) axis -= 3;
         lind_axis[off] = axis;
         if (axis >= 4 && axis <= 6) {  // QUADAA layout (rt2_layout.h)
           const float n[3] = {r[0], r[1], r[2]}, d = r[3], q[3] = {r[4], r[5], r[6]}, mat = r[7];

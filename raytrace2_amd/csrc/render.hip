@@ -936,6 +936,10 @@ __device__ __forceinline__ bool quad_cand_w(const float* w, f3 o, f3 d, float& t
 // dot(n, d), dot(n, o) and dot(w, cross(., .)) equal the single axis-K products in value (the
 // other terms are signed zeros, which no comparison distinguishes), so this returns the same
 // decision and t as quad_cand_w at a third of the arithmetic.
+// The float above 1e-8f: |n.d| > 1e-8f, the quads' parallel-ray rejection (Quad.cpp:22, |denom| < 1e-8
+// in double, is |denom| <= 1e-8f for a float denom), as |n.d| >= kAboveDenomMin
+constexpr float kAboveDenomMin = 0x1.5798f0p-27f;
+static_assert(kAboveDenomMin > 1e-8f && 0x1.5798eep-27f == 1e-8f, "the float after 1e-8f");
 template <int K>
 __device__ __forceinline__ float comp(f3 v) {
   return K == 0 ? v.x : (K == 1 ? v.y : v.z);
@@ -980,20 +984,26 @@ __device__ __forceinline__ bool in_interval(float t, float lo, float hi) {
 // (r.at(t)), and the interior test alpha, beta in [0, 1] as lo <= p <= hi on each coordinate: the
 // compiler records rectangles only, whose alpha depends on p[A] alone through monotone rounded
 // operations and beta on p[B] alone, and the bounds are the first and last floats it accepts
-// (compile.cpp CoordRange), so the decision is the same for every p, NaN and +-inf rejected.
+// (compile.cpp CoordRange), so the decision is the same for every finite p.
+// Returned as a rejection word whose sign bit is set when the quad is not hit: the sign of a rounded
+// difference is the sign of the exact one (a zero only for equal operands, +0 then; lo is stored as -0
+// where it is 0, so p = -0 passes as p = +0 does), so p - lo, hi - p, ... are all >= 0 exactly when p
+// is inside, and |d_K| - (the float above 1e-8f) >= 0 exactly when |d_K| > 1e-8f (Quad.cpp:22:
+// |denom| < 1e-8, in double). One OR of the words and one sign test instead of five compare masks
+// and their scalar ANDs: the lockstep kernels' scalar unit is as busy as their vector pipes. (The ray's
+// o and d are finite, so t and p are: compile.cpp RectAAWords bounds the scene.)
 template <int K>
-__device__ __forceinline__ bool quad_aa(const float* r, f3 o, f3 d, f3 inv, float& t_out) {
+__device__ __forceinline__ uint32_t quad_aa(const float* r, f3 o, f3 d, f3 inv, float& t_out) {
   constexpr int A = (K + 1) % 3, B = (K + 2) % 3;
   const float dk = comp<K>(d);
   const float t = div_by_inv(r[0] - comp<K>(o), dk, comp<K>(inv));
   const float pa = comp<A>(o) + comp<A>(d) * t;
   const float pb = comp<B>(o) + comp<B>(d) * t;
   t_out = t;
-  // (bitwise: both coordinates are tested for every lane, no divergent branch)
-  return (int)!(fabsf(dk) <= 1e-8f) & (int)(r[1] <= pa) & (int)(pa <= r[2]) & (int)(r[3] <= pb) &
-         (int)(pb <= r[4]);
+  return (__float_as_uint(pa - r[1]) | __float_as_uint(r[2] - pa) | __float_as_uint(pb - r[3])) |
+         (__float_as_uint(r[4] - pb) | __float_as_uint(fabsf(dk) - kAboveDenomMin));
 }
-__device__ __forceinline__ bool quad_aa_k(uint32_t k, const float* r, f3 o, f3 d, f3 inv, float& t) {
+__device__ __forceinline__ uint32_t quad_aa_k(uint32_t k, const float* r, f3 o, f3 d, f3 inv, float& t) {
   if (k == 0u) return quad_aa<0>(r, o, d, inv, t);
   if (k == 1u) return quad_aa<1>(r, o, d, inv, t);
   return quad_aa<2>(r, o, d, inv, t);
@@ -1168,8 +1178,8 @@ __device__ __forceinline__ bool quad_aa_div(const uint32_t* r, f3 o, f3 d, float
   const float pa = comp<A>(o) + comp<A>(d) * t;
   const float pb = comp<B>(o) + comp<B>(d) * t;
   t_out = t;
-  return (int)!(fabsf(dk) <= 1e-8f) & (int)(uf(r[1]) <= pa) & (int)(pa <= uf(r[2])) & (int)(uf(r[3]) <= pb) &
-         (int)(pb <= uf(r[4]));
+  return (int)((__float_as_uint(pa - uf(r[1])) | __float_as_uint(uf(r[2]) - pa) | __float_as_uint(pb - uf(r[3]))) |
+               (__float_as_uint(uf(r[4]) - pb) | __float_as_uint(fabsf(dk) - kAboveDenomMin))) >= 0;
 }
 // Both boundary queries of ConstantMedium::Hit (ConstantMedium.cpp:14-58) on a box in one pass:
 // each quad's t and interior decision do not depend on the query's interval, so its quads are
@@ -1547,7 +1557,7 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
         const uint32_t o0 = off + 5u * k;
         const uint32_t c0 = codes & 7u;
         float t0;
-        bool ok0;
+        uint32_t rej;  // sign bit set: no candidate (quad_aa)
         uint32_t kind0;
         if (c0 >= 4u) {
           const u32x8 a = k == 0u ? u32x8{sw[4], sw[5], sw[6], sw[7], sw[8], sw[9], sw[10], sw[11]}
@@ -1555,7 +1565,7 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
           float ra[8];
 #pragma unroll
           for (int j = 0; j < 8; j++) ra[j] = uf(a[j]);
-          ok0 = quad_aa_k(c0 - 4u, ra, o, d, inv, t0);
+          rej = quad_aa_k(c0 - 4u, ra, o, d, inv, t0);
           kind0 = kQuadAA;
         } else {
           u32x16 a;
@@ -1566,7 +1576,7 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
           for (int j = 0; j < 16; j++) w0[j] = uf(a[j]);
 #pragma unroll
           for (int j = 0; j < 4; j++) w0[16 + j] = uf(b2[j]);
-          ok0 = quad_cand_u(c0, w0, o, d, inv, t0);
+          rej = quad_cand_u(c0, w0, o, d, inv, t0) ? 0u : 0x80000000u;
           kind0 = kQuad;
         }
         if (kStats) cnt.quad += 1;
@@ -1581,13 +1591,15 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
             float ra[8];
 #pragma unroll
             for (int j = 0; j < 8; j++) ra[j] = uf(a[j]);
-            ok2 = quad_aa_k(c0 - 4u, ra, o2, d, inv, t2);
+            ok2 = (int)quad_aa_k(c0 - 4u, ra, o2, d, inv, t2) >= 0;
           }
           asm volatile("" ::"v"(t2), "v"((int)ok2));
         }
 #endif
+        // kt <= kmax (unsigned) as the sign of kt | (kmax - kt): kmax < 2^31 (a key of a t in [tmin,
+        // FLT_MAX]); a kt >= 2^31 is rejected by its own sign, a smaller one by the difference's
         const uint32_t kt = bits(t0) - bits(tmin);
-        if (ok0 & (kt <= kmax)) {
+        if ((int)(rej | kt | (kmax - kt)) >= 0) {
           kmax = kt;
           prim = make_ref(kind0, o0);
         }

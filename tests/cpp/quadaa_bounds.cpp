@@ -3,7 +3,8 @@
 // For random axis-aligned rectangles of every orientation (u along A or along B, both normal signs,
 // corners and edges from tiny to huge, exact zeros), built as Quad's constructor builds them
 // (Quad.cpp:6-17: n = cross(u, v), D = dot(normal, q), w = n / dot(n, n)), the kernel's decision
-// lo[A] <= p[A] <= hi[A] && lo[B] <= p[B] <= hi[B] must equal Quad::Hit's interior test
+// lo[A] <= p[A] <= hi[A] && lo[B] <= p[B] <= hi[B], and its sign-word form (render.hip quad_aa),
+// must equal Quad::Hit's interior test
 // (Quad.cpp:27-36: alpha = dot(w, cross(pv, v)), beta = dot(w, cross(u, pv)), pv = p - q, both in
 // [0, 1]) for hit points p around and on the bounds, at +-0, +-inf, NaN and far away, off the plane by
 // rounding (compile.cpp RectAAWords: corners and edges within +-2^40, ray origins within +-2^80). Prints the
@@ -28,6 +29,11 @@ float dot(V3 a, V3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
 V3 cross(V3 x, V3 y) { return {x.y * y.z - y.y * x.z, x.z * y.x - y.z * x.x, x.x * y.y - y.x * x.y}; }
 V3 sub(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
 
+uint32_t Bits(float f) {
+  uint32_t b;
+  memcpy(&b, &f, 4);
+  return b;
+}
 bool reference_inside(V3 p, V3 q, V3 u, V3 v, V3 w) {
   const V3 pv = sub(p, q);
   const float alpha = dot(w, cross(pv, v)), beta = dot(w, cross(u, pv));
@@ -100,8 +106,12 @@ int main(int argc, char** argv) {
         p[k] = (rng() & 3) == 0 ? q[k] : q[k] + off;
         const bool ref = reference_inside(p, q, u, v, w);
         const bool got = lo[0] <= p[a] && p[a] <= hi[0] && lo[1] <= p[b] && p[b] <= hi[1];
+        // the kernel's form (render.hip quad_aa): the sign bits of the four rounded differences, for
+        // every non-NaN p (a NaN p needs a non-finite ray, which the kernel never traces)
+        const uint32_t rej = Bits(p[a] - lo[0]) | Bits(hi[0] - p[a]) | Bits(p[b] - lo[1]) | Bits(hi[1] - p[b]);
+        const bool got_word = (rej >> 31) == 0u;
         compared++;
-        if (ref != got) {
+        if (ref != got || (!std::isnan(p[a]) && !std::isnan(p[b]) && ref != got_word)) {
           std::fprintf(stderr,
                        "mismatch: k=%d along_b=%d q=(%a %a %a) eu=%a ev=%a p=(%a %a %a) ref=%d got=%d bounds A [%a %a] B "
                        "[%a %a]\n",

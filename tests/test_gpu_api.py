@@ -40,6 +40,21 @@ def test_invalid_arguments_fail_loudly_and_keep_the_tracer(tracer, call):
     assert tracer.FrameIdx() == 2 and np.isfinite(tracer.NonConvertedPixels()).all()
 
 
+def test_camera_beyond_the_exact_range_fails_loudly(tracer):
+    """The rectangle test is exact for ray origins within +-2^100 (compile.cpp RectAAWords): a camera
+    whose rays would start beyond +-2^64 (capi.cpp CameraOriginsBounded) is refused at Render with
+    RT2_ERR_INVALID, and the tracer renders again once the camera is back in range."""
+    import dataclasses
+    good = tracer.get_camera()
+    tracer.set_camera(dataclasses.replace(good, center=(1e30, 278.0, -800.0)))
+    with pytest.raises(Rt2Error) as e:
+        tracer.Render(1)
+    assert "2^64" in str(e.value)
+    tracer.set_camera(good)
+    tracer.Render(2)
+    assert tracer.FrameIdx() == 2 and np.isfinite(tracer.NonConvertedPixels()).all()
+
+
 def test_queued_frames_and_reset(tracer):
     for _ in range(5):
         tracer.Update()
