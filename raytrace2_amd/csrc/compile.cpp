@@ -867,9 +867,12 @@ bool CompileSceneWith(const Scene& s, CompiledScene& out, std::string& err, bool
   }
   // Wide program: each 16-byte step entry followed by the first 48 bytes of its record (a whole BVH
   // node or QUADAA quad), so one 64-byte scalar load fetches both
+  // plus one entry past the last step, kind kProgramEnd: the wave's next step index reaches n when
+  // every lane is done, and the kernel reads that entry's kind instead of comparing the index with n
   {
     size_t n = out.lin.size() / 4;
-    out.lin_wide.assign(16 * n, 0u);
+    out.lin_wide.assign(16 * (n + 1), 0u);
+    out.lin_wide[16 * n] = kProgramEnd;
     for (size_t i = 0; i < n; i++) {
       for (int k = 0; k < 4; k++) out.lin_wide[16 * i + k] = out.lin[4 * i + k];
       const size_t rec = 4 * (size_t)out.lin[4 * i + 2];

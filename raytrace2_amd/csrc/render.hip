@@ -1480,13 +1480,13 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
   f3 acc_pinv = mk(0.0f, 0.0f, 0.0f);  // accelerated list: this ray's box padding x inv
   uint32_t acc_best = kRefNone;  // accelerated list: child index of its current closest sphere
   uint32_t next = 0;  // this lane's next step
-  const uint32_t len = P.lin_len;
   RT2_WAVE(0);
 #if RT2_EXP_WAVESTEPS
   cnt.wd[7]++;
 #endif
   uint32_t i = wave_min_next(next);  // wave-uniform step = min over live lanes of `next`
-  while (i < len) {
+  // (i reaches P.lin_len when every lane is done: the wide program's entry there is kProgramEnd)
+  while (true) {
     u32x16 sw = sld16(P.lin_wide, i * 64u);  // entry + the first 48 bytes of its record
     if (sw[0] == kBvh) {
       // A run of BVH steps in a loop of their own: only `next` changes from step to step, so
@@ -1529,13 +1529,12 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
           next = kSel && !act ? next : nx;
         }
         i = wave_min_next(next);
-        if (i >= len) break;
         sw = sld16(P.lin_wide, i * 64u);
       } while (sw[0] == kBvh);
-      if (i >= len) break;
     }
     const u32x4 st = {sw[0], sw[1], sw[2], sw[3]};
     const uint32_t kind = st.x, off = st.z;
+    if (kind == kProgramEnd) break;
     RT2_WAVE(1);
     if (kind == kQuad) RT2_WAVE(3);
     if (is_acc_bvh(kind)) RT2_WAVE(2);

@@ -28,6 +28,7 @@ enum NodeKind : uint32_t {
   kAccBvh = 8,     // 8 + split axis (8, 9, 10): node of a list's acceleration tree
   kAccSphere = 11, // a sphere reached through a list's acceleration tree
   kQuadAA = 12,    // threaded program only: a unit-normal axis-aligned quad in the QUADAA layout
+  kProgramEnd = 13,  // threaded program only: the wide program's entry at index lin_len (no step)
 };
 inline constexpr bool is_acc_bvh(uint32_t kind) { return kind - kAccBvh < 3u; }
 constexpr int kListAccelMin = 32;  // leaf-only sphere lists at least this long get a tree

@@ -149,7 +149,8 @@ struct CompiledScene {
   uint32_t features = 0;          // rt2_layout.h Feature bits (defocus is added per render)
   std::vector<uint32_t> lin;      // threaded traversal program (4 words per step), empty if too long
   std::vector<float> lind;        // records of the program's steps, in program order (float4)
-  std::vector<uint32_t> lin_wide; // 16 words per step: the lin entry + the first 12 words of its record
+  std::vector<uint32_t> lin_wide; // 16 words per step: the lin entry + the first 12 words of its record,
+                                  // then one kProgramEnd entry
 };
 // accelerate_lists = false keeps every list a linear child loop (the reference's own order).
 bool CompileScene(const Scene& s, CompiledScene& out, std::string& err, bool accelerate_lists = true);

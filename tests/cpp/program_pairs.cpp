@@ -35,7 +35,8 @@ int main(int argc, char** argv) {
     return 2;
   }
   const size_t n = c.lin.size() / 4;
-  if (n == 0 || c.lin_wide.size() != 16 * n) return fail("no wide program", 0);
+  if (n == 0 || c.lin_wide.size() != 16 * (n + 1)) return fail("no wide program", 0);
+  if (c.lin_wide[16 * n] != kProgramEnd) return fail("no kProgramEnd entry after the last step", n);
   std::vector<char> target(n + 1, 0), second(n + 1, 0);
   for (size_t i = 0; i < n; i++) {
     const uint32_t k = c.lin[4 * i];
