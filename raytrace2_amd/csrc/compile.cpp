@@ -857,12 +857,14 @@ bool CompileSceneWith(const Scene& s, CompiledScene& out, std::string& err, bool
         run = std::min(out.lin[4 * (i + 1) + 3] + 1, kLinearMaxRun);
       out.lin[4 * i + 3] = run;
     }
-    // axis codes of each run's quads, 3 bits each, in the skip word
+    // axis codes of each run's quads, 3 bits each, then a 1 bit (the kernel's loop ends when the
+    // codes shifted past the last quad equal 1), in the skip word
     for (size_t i = 0; i < n; i++) {
       if (out.lin[4 * i] != kQuad) continue;
       uint32_t codes = 0;
-      for (uint32_t k = 0; k < out.lin[4 * i + 3]; k++) codes |= fl.lind_axis.at(out.lin[4 * (i + k) + 2]) << (3 * k);
-      out.lin[4 * i + 1] = codes;
+      const uint32_t run = out.lin[4 * i + 3];
+      for (uint32_t k = 0; k < run; k++) codes |= fl.lind_axis.at(out.lin[4 * (i + k) + 2]) << (3 * k);
+      out.lin[4 * i + 1] = codes | (1u << (3 * run));
     }
   }
   // Wide program: each 16-byte step entry followed by the first 48 bytes of its record (a whole BVH

@@ -1548,35 +1548,46 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
       // a run of st.w quads with contiguous records, axis codes in st.y (3 bits each), tested in
       // order (issue-bound: one candidate at a time beats two interleaved, measured)
       const uint32_t run = st.w;
-      uint32_t codes = st.y;
+      uint32_t codes = st.y;  // 3 bits per quad, then a 1 bit (compile.cpp)
       // the run's interval test in_interval(t, tmin, tmax) as key(t) <= kmax with key(x) = bits(x) -
       // bits(tmin) (kmax = key(tmax), updated with the accepted t's key; tmax = its float after the run)
       uint32_t kmax = bits(tmax) - bits(tmin);
-      for (uint32_t k = 0; k < run; k++, codes >>= 3) {
-        const uint32_t o0 = off + 5u * k;
+      uint32_t boff = off * 16u;  // byte offset of the quad's record
+      // the quad's QUADAA ref, counted in a VGPR (one VALU add per quad instead of two scalar
+      // instructions and a copy to build each accepted ref: the scalar unit is the busier pipe)
+      uint32_t vref = make_ref(kQuadAA, off);
+      asm volatile("" : "+v"(vref));
+      for (bool first = true;; first = false) {
         const uint32_t c0 = codes & 7u;
         float t0;
-        uint32_t rej;  // sign bit set: no candidate (quad_aa)
-        uint32_t kind0;
+        // kt <= kmax (unsigned) as the sign of kt | (kmax - kt): kmax < 2^31 (a key of a t in [tmin,
+        // FLT_MAX]); a kt >= 2^31 is rejected by its own sign, a smaller one by the difference's
         if (c0 >= 4u) {
-          const u32x8 a = k == 0u ? u32x8{sw[4], sw[5], sw[6], sw[7], sw[8], sw[9], sw[10], sw[11]}
-                                  : sld8(recs, o0 * 16u);
+          const u32x8 a = first ? u32x8{sw[4], sw[5], sw[6], sw[7], sw[8], sw[9], sw[10], sw[11]} : sld8(recs, boff);
           float ra[8];
 #pragma unroll
           for (int j = 0; j < 8; j++) ra[j] = uf(a[j]);
-          rej = quad_aa_k(c0 - 4u, ra, o, d, inv, t0);
-          kind0 = kQuadAA;
+          const uint32_t rej = quad_aa_k(c0 - 4u, ra, o, d, inv, t0);  // sign bit set: no candidate
+          const uint32_t kt = bits(t0) - bits(tmin);
+          if ((int)(rej | kt | (kmax - kt)) >= 0) {
+            kmax = kt;
+            prim = vref;
+          }
         } else {
           u32x16 a;
           u32x4 b2;
-          sld20(recs, o0 * 16u, a, b2);
+          sld20(recs, boff, a, b2);
           float w0[20];
 #pragma unroll
           for (int j = 0; j < 16; j++) w0[j] = uf(a[j]);
 #pragma unroll
           for (int j = 0; j < 4; j++) w0[16 + j] = uf(b2[j]);
-          rej = quad_cand_u(c0, w0, o, d, inv, t0) ? 0u : 0x80000000u;
-          kind0 = kQuad;
+          const bool ok0 = quad_cand_u(c0, w0, o, d, inv, t0);
+          const uint32_t kt = bits(t0) - bits(tmin);
+          if (ok0 && kt <= kmax) {
+            kmax = kt;
+            prim = vref ^ ((kQuadAA ^ kQuad) << 28);  // the QUAD layout's kind
+          }
         }
         if (kStats) cnt.quad += 1;
 #if RT2_EXP_TWICE & 16
@@ -1586,7 +1597,7 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
           float t2 = 0.0f;
           bool ok2 = false;
           if (c0 >= 4u) {
-            const u32x8 a = sld8(recs, o0 * 16u);
+            const u32x8 a = sld8(recs, boff);
             float ra[8];
 #pragma unroll
             for (int j = 0; j < 8; j++) ra[j] = uf(a[j]);
@@ -1595,13 +1606,10 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
           asm volatile("" ::"v"(t2), "v"((int)ok2));
         }
 #endif
-        // kt <= kmax (unsigned) as the sign of kt | (kmax - kt): kmax < 2^31 (a key of a t in [tmin,
-        // FLT_MAX]); a kt >= 2^31 is rejected by its own sign, a smaller one by the difference's
-        const uint32_t kt = bits(t0) - bits(tmin);
-        if ((int)(rej | kt | (kmax - kt)) >= 0) {
-          kmax = kt;
-          prim = make_ref(kind0, o0);
-        }
+        codes >>= 3;
+        if (codes == 1u) break;
+        boff += 16u * (uint32_t)kQuadRecords;
+        vref += (uint32_t)kQuadRecords;
       }
       tmax = uf(kmax + bits(tmin));
       next = at + run;

@@ -159,7 +159,7 @@ constexpr int kLdsSceneBytesMax = 96 * 1024;  // scenes up to this size are stag
 //   kind kQuad / kSphere / kMedium: record of the primitive; the next step is always index + 1;
 //     for kQuad, aux = length of the run of consecutive quads starting here (at most
 //     kLinearMaxRun) with no skip target inside it, skip = the run's axis codes, 3 bits per quad
-//     (codes 4..6 use the QUADAA record layout, the others the QUAD layout)
+//     (codes 4..6 use the QUADAA record layout, the others the QUAD layout), then a 1 bit
 //   kind kXform: enter the transform (record = XFORM record, skip = index of its kXformExit);
 //     the kernel walks the steps up to the exit in a nested loop with the transformed ray
 //   kind kXformExit: leave it (record = XFORM record, aux = parent XFORM ref or kRefNone, skip = the end
@@ -182,7 +182,8 @@ constexpr int kLinearMaxSteps = 1 << 16;
 #ifndef RT2_LINEAR_MAX_RUN
 #define RT2_LINEAR_MAX_RUN 10
 #endif
-constexpr uint32_t kLinearMaxRun = RT2_LINEAR_MAX_RUN;  // quads per run (3-bit axis codes in one word)
+constexpr uint32_t kLinearMaxRun = RT2_LINEAR_MAX_RUN;  // quads per run (3-bit axis codes + 1 bit in one word)
+static_assert(3 * kLinearMaxRun < 32, "a run's codes and their end bit fit one word");
 constexpr int kLinearMaxXformDepth = 8;  // deeper transform nesting uses the stack traversal
 
 // kModeStackHybrid: the scene is too large for LDS, but its BVH node records (the prefix
