@@ -917,6 +917,8 @@ bool CompileSceneWith(const Scene& s, CompiledScene& out, std::string& err, bool
   PackMaterials(s, out);
   PackTextures(s, out);
   if (out.spheres) out.features |= kFeatSphere;
+  for (const Obj& o : s.objs)
+    if (o.kind == kSphere && !(o.disp.x == 0.0f && o.disp.y == 0.0f && o.disp.z == 0.0f)) out.features |= kFeatMotion;
   if (out.media) out.features |= kFeatMedium;
   if (out.xforms) out.features |= kFeatXform;
   if (out.acc_lists) out.features |= kFeatAccList;

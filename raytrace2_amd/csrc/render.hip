@@ -866,10 +866,11 @@ __device__ __forceinline__ bool sphere_fast_ok_pos(float a, float hh, float sq) 
 // roots when every lane of the wave is in sphere_fast_ok_pos's range (queries with tmin >= 0.001);
 // 4: in sphere_fast_ok's (any interval: a medium's boundary queries); 1 / 3: when this lane is in
 // sphere_fast_ok's / sphere_fast_ok_pos's range (selftest); 2: IEEE division only (selftest reference).
-template <int kDiv = 0>
+// kMotion false (kernels for scenes whose spheres all stand still, kFeatMotion): center(time) = c0.
+template <int kDiv = 0, bool kMotion = true>
 __device__ __forceinline__ bool sphere_t_rec(float4 r0, float4 r1, f3 o, f3 d, float time, float tmin, float tmax,
                                              float& t_out) {
-  f3 center = xyz(r0) + xyz(r1) * time;
+  const f3 center = kMotion ? xyz(r0) + xyz(r1) * time : xyz(r0);
   f3 oc = center - o;
   float a = dot(d, d);
   float hh = dot(d, oc);
@@ -894,10 +895,10 @@ __device__ __forceinline__ bool sphere_t_rec(float4 r0, float4 r1, f3 o, f3 d, f
   t_out = root;
   return true;
 }
-template <int kMode, int kDiv = 0>
+template <int kMode, int kDiv = 0, bool kMotion = true>
 __device__ __forceinline__ bool sphere_t(const Nodes<kMode>& N, uint32_t off, f3 o, f3 d, float time, float tmin,
                                          float tmax, float& t_out) {
-  return sphere_t_rec<kDiv>(N[off], N[off + 1], o, d, time, tmin, tmax, t_out);
+  return sphere_t_rec<kDiv, kMotion>(N[off], N[off + 1], o, d, time, tmin, tmax, t_out);
 }
 
 // Quad::Hit split in two: the candidate (pure function of the ray) and the interval test. The
@@ -1030,7 +1031,7 @@ __device__ __forceinline__ bool prim_t(const Nodes<kMode>& N, uint32_t ref, f3 o
   if constexpr (Has<F, kFeatSphere>()) {
     if ((ref >> 28) == kSphere) {
       cnt.sphere++;
-      return sphere_t<kMode, kBoundary ? 4 : 0>(N, off, o, d, time, tmin, tmax, t);
+      return sphere_t<kMode, kBoundary ? 4 : 0, Has<F, kFeatMotion>()>(N, off, o, d, time, tmin, tmax, t);
     }
   }
   cnt.quad++;
@@ -1117,8 +1118,8 @@ __device__ __forceinline__ bool boundary_prim_lin(const void* recs, uint32_t ref
   const uint32_t off = ref & kOffsetMask;
   if (Has<F, kFeatSphere>() && (ref >> 28) == kSphere) {
     cnt.sphere++;
-    return sphere_t<kModeLinear, 4>(Nodes<kModeLinear>{reinterpret_cast<const float4*>(recs), 0u}, off, o, d, time, lo,
-                                    hi, t_out);
+    return sphere_t<kModeLinear, 4, Has<F, kFeatMotion>()>(Nodes<kModeLinear>{reinterpret_cast<const float4*>(recs), 0u},
+                                                             off, o, d, time, lo, hi, t_out);
   }
   cnt.quad++;
   u32x16 a;
@@ -1423,7 +1424,7 @@ __device__ __forceinline__ bool trace_stack(const RenderParams& P, const Nodes<k
       // smallest root wins; an equal root goes to the lower child index = lower record offset
       if (kStats) cnt.sphere++;
       float t;
-      if (sphere_t(N, off, o, d, time, tmin, FLT_MAX, t) &&
+      if (sphere_t<kMode, 0, Has<F, kFeatMotion>()>(N, off, o, d, time, tmin, FLT_MAX, t) &&
           (t < tmax || (t == tmax && acc_best != kRefNone && off < acc_best))) {
         tmax = t;
         any = true;
@@ -1618,7 +1619,7 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
       uint32_t ref = make_ref(kind, off);
       // the sphere record (c0, r | disp, mat) is the step's inline words: no load
       if (kStats) cnt.sphere++;
-      const bool hs = sphere_t_rec(make_float4(uf(sw[4]), uf(sw[5]), uf(sw[6]), uf(sw[7])),
+      const bool hs = sphere_t_rec<0, Has<F, kFeatMotion>()>(make_float4(uf(sw[4]), uf(sw[5]), uf(sw[6]), uf(sw[7])),
                                    make_float4(uf(sw[8]), uf(sw[9]), uf(sw[10]), uf(sw[11])), o, d, time, tmin, tmax, t);
       if (hs) {
         tmax = t;
@@ -1739,7 +1740,7 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
           } else {  // ACCSPHERE: the record's words inline, aux = list position
             if (kStats) cnt.sphere++;
             float t;
-            if (sphere_t_rec(make_float4(uf(e1.x), uf(e1.y), uf(e1.z), uf(e1.w)),
+            if (sphere_t_rec<0, Has<F, kFeatMotion>()>(make_float4(uf(e1.x), uf(e1.y), uf(e1.z), uf(e1.w)),
                              make_float4(uf(e2.x), uf(e2.y), uf(e2.z), uf(e2.w)), o, d, time, tmin, FLT_MAX, t) &&
                 (t < tmax || (t == tmax && acc_best != kRefNone && e0.w < acc_best))) {
               tmax = t;
@@ -1810,7 +1811,7 @@ __device__ __forceinline__ void resolve_hit(const Nodes<kMode>& N, const HitRef&
     mat = N.word(off, 1);
   } else if (Has<F, kFeatSphere>() && kind == kSphere) {
     float4 r0 = N[off], r1 = N[off + 1];
-    f3 center = xyz(r0) + xyz(r1) * time;
+    const f3 center = Has<F, kFeatMotion>() ? xyz(r0) + xyz(r1) * time : xyz(r0);
     f3 outward = (p - center) / r0.w;
     front = dot(d, outward) < 0.0f;
     n = front ? outward : -outward;
@@ -1994,7 +1995,7 @@ __device__ __forceinline__ uint32_t local_index(const LoopArgs& A, uint32_t x, u
 template <uint32_t F, int kMode, bool kStats>
 constexpr int MinWaves() {
   if (RT2_MIN_WAVES_PER_EU > 0) return RT2_MIN_WAVES_PER_EU;
-  constexpr uint32_t kBook2 = kFeatSphere | kFeatMedium | kFeatXform | kFeatNoise | kFeatSpecular | kFeatAccList;
+  constexpr uint32_t kBook2 = kFeatSphere | kFeatMedium | kFeatXform | kFeatNoise | kFeatSpecular | kFeatAccList | kFeatMotion;
   if ((F == kFeatAll || F == kBook2) && !kStats && (kMode == kModeStackGlobal || kMode == kModeStackHybrid))
     return RT2_MIN_WAVES_ALL;  // book 2
   if (F == kBook2 && !kStats && kMode == kModeLinear) return RT2_MIN_WAVES_B2LIN;
@@ -2024,7 +2025,7 @@ constexpr bool LdsRng() {
 // stores: staging measured no faster for it), which leaves the LDS room for the park planes.
 template <uint32_t F, int kMode, bool kStats>
 constexpr bool Park() {
-  constexpr uint32_t kBook2 = kFeatSphere | kFeatMedium | kFeatXform | kFeatNoise | kFeatSpecular | kFeatAccList;
+  constexpr uint32_t kBook2 = kFeatSphere | kFeatMedium | kFeatXform | kFeatNoise | kFeatSpecular | kFeatAccList | kFeatMotion;
   return F == kBook2 && kMode == kModeLinear && !kStats && LdsRng<F, kMode, kStats>();
 }
 // Kernels whose threaded medium step takes both box-boundary queries in one pass (boundary_aa_pair):
@@ -2563,7 +2564,7 @@ constexpr uint32_t kVariants[] = {
     kFeatXform,                                   // Cornell box
     kFeatXform | kFeatMedium,                     // Cornell volume
     kFeatSphere | kFeatSpecular | kFeatDefocus,   // RTIOW book 1
-    kFeatSphere | kFeatMedium | kFeatXform | kFeatNoise | kFeatSpecular | kFeatAccList,  // RTNW book 2
+    kFeatSphere | kFeatMedium | kFeatXform | kFeatNoise | kFeatSpecular | kFeatAccList | kFeatMotion,  // RTNW book 2
     kFeatAll,                                     // everything (scene graphs, checker textures)
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);

@@ -140,7 +140,7 @@ constexpr int kTraversalStack = 24;  // max entries per lane (LDS); compile.cpp 
 // smallest instantiated superset of the scene's features, so code (and registers) for absent
 // features is not compiled into the kernel that runs.
 enum Feature : uint32_t {
-  kFeatSphere = 1u << 0,    // Sphere primitives (incl. motion)
+  kFeatSphere = 1u << 0,    // Sphere primitives
   kFeatMedium = 1u << 1,    // ConstantMedium + Isotropic
   kFeatXform = 1u << 2,     // TransformedHittable
   kFeatNoise = 1u << 3,     // Noise (Perlin / marble) textures
@@ -149,7 +149,9 @@ enum Feature : uint32_t {
   kFeatDefocus = 1u << 6,   // thin-lens camera (defocus_angle > 0)
   kFeatGenList = 1u << 7,   // lists whose children are not all quads/spheres (pushed on the stack)
   kFeatAccList = 1u << 8,   // accelerated sphere lists (LISTACC)
-  kFeatAll = 0x1FFu,
+  kFeatMotion = 1u << 9,    // a sphere that moves (displacement not +-0); without it the kernel
+                            // takes center(time) = c0 (c0 + (+-0) differs only in a zero's sign)
+  kFeatAll = 0x3FFu,
 };
 constexpr int kLdsSceneBytesMax = 96 * 1024;  // scenes up to this size are staged in LDS
 

@@ -108,7 +108,7 @@ def test_book2_bench_kernel_spills_stay_out_of_the_trace(isa):
     §4): its scratch stays at most 96 B per lane and no spill store or reload sits inside the trace's
     loops (loop depth >= 2); the reloads left are the marble texture's double-precision sin constants
     on the shading path (depth 1)."""
-    scratch, body = _kernel(isa, "ILj303ELi2ELb0E")
+    scratch, body = _kernel(isa, "ILj815ELi2ELb0E")
     deep = [x for x in _loop_depth_scratch(body) if x[0] >= 2]
     assert scratch <= 96 and not deep, (scratch, deep[:5])
 
