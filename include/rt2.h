@@ -159,7 +159,9 @@ RT2_API int rt2_tracer_copy_accum_device(rt2_tracer* tr, void* dst_device, void*
  * frame and does not reset the accumulation. set_camera gives the tracer the setter fields of
  * Camera.hpp:69-101 (center, look_at, view_up, vfov, defocus_angle, focus_distance; dims and
  * samples_per_pixel stay as on_resize / set_samples_per_pixel set them). When they change, frames
- * queued so far are launched first, with the camera they were queued under. */
+ * queued so far are launched first, with the camera they were queued under. Rendering refuses, with
+ * RT2_ERR_INVALID, a camera whose rays would start beyond +-2^64 on an axis (center plus the defocus
+ * disk): the kernel's exact axis-aligned rectangle test assumes ray origins within +-2^100. */
 RT2_API int rt2_tracer_set_camera(rt2_tracer* tr, const rt2_camera_desc* cam);
 RT2_API int rt2_tracer_get_camera(const rt2_tracer* tr, rt2_camera_desc* out);
 
