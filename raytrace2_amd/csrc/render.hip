@@ -1561,19 +1561,18 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
       for (bool first = true;; first = false) {
         const uint32_t c0 = codes & 7u;
         float t0;
-        // kt <= kmax (unsigned) as the sign of kt | (kmax - kt): kmax < 2^31 (a key of a t in [tmin,
-        // FLT_MAX]); a kt >= 2^31 is rejected by its own sign, a smaller one by the difference's
+        // kmax < 2^31 (a key of a t in [tmin, FLT_MAX]): a candidate whose key or rejection word has
+        // the sign bit set is never <= kmax
         if (c0 >= 4u) {
           const u32x8 a = first ? u32x8{sw[4], sw[5], sw[6], sw[7], sw[8], sw[9], sw[10], sw[11]} : sld8(recs, boff);
           float ra[8];
 #pragma unroll
           for (int j = 0; j < 8; j++) ra[j] = uf(a[j]);
           const uint32_t rej = quad_aa_k(c0 - 4u, ra, o, d, inv, t0);  // sign bit set: no candidate
-          const uint32_t kt = bits(t0) - bits(tmin);
-          if ((int)(rej | kt | (kmax - kt)) >= 0) {
-            kmax = kt;
-            prim = vref;
-          }
+          // kt with the rejection's sign bit: <= kmax (< 2^31) exactly for an accepted candidate
+          const uint32_t x = (bits(t0) - bits(tmin)) | (rej & 0x80000000u);
+          if (x <= kmax) prim = vref;
+          kmax = min(kmax, x);
         } else {
           u32x16 a;
           u32x4 b2;
@@ -1839,6 +1838,8 @@ __device__ __forceinline__ void resolve_hit(const Nodes<kMode>& N, const HitRef&
     // back through every enclosing transform, innermost first (Transform.cpp:85-86)
     for (uint32_t x = h.xf; x != kRefNone;) {
       uint32_t xo = x & kOffsetMask;
+      // (the parent link with M: the loop's exit test does not wait on a load of its own)
+      const float4 c1 = N[xo + 1];
       float4 m0 = N[xo + 4], m1 = N[xo + 5], m2 = N[xo + 6], m3 = N[xo + 7];
       // (c2.w: the transform's pattern in the threaded program's copy, 0 in the node array)
       if (kMode == kModeLinear && N.word(xo + 2, 3) == kXformYAxis) {  // M's +-0 products left out
@@ -1848,7 +1849,6 @@ __device__ __forceinline__ void resolve_hit(const Nodes<kMode>& N, const HitRef&
                (m0.z * p.x + m1.z * p.y) + (m2.z * p.z + m3.z));
       }
       // (a medium's hit normal is never read: Isotropic::Scatter ignores it, Material.cpp:76-83)
-      const float4 c1 = N[xo + 1];
       if (!(Has<F, kFeatMedium>() && kind == kMedium) && !wnormal) {
         const float4 c0 = N[xo], c2 = N[xo + 2];
         n = normalize(mk(c0.x * n.x + c0.y * n.y + c0.z * n.z, c1.x * n.x + c1.y * n.y + c1.z * n.z,
