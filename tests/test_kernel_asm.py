@@ -156,18 +156,18 @@ def test_cornell_quad_run_loop_keeps_the_scalar_issue_code_generation(isa):
     branches; -simplifycfg-sink-common=false keeps the three per-axis QUADAA bodies apart instead of one
     body fed by register copies). A toolchain that silently changed what they do would cost ~16 % with
     every other test green; this guard fails instead. The Cornell kernel's quad-run loop (the depth-3 loop
-    with a scalar record load whose QUADAA test ORs its rejection words with v_or3: two per axis body, one
-    for the interval key) must hold three separate interior tests (7 v_or3; one merged body: 3), no
-    exec-mask save per quad, and at most 32 SALU instructions (with the options: 26; without them: 47);
-    its trace loop at most 150 SALU (131; without: 175)."""
+    with a scalar record load whose QUADAA test ORs its rejection words with v_or3, two per axis body)
+    must hold three separate interior tests (6 v_or3; one merged body: 2), no exec-mask save per quad,
+    and at most 28 SALU instructions (with the options: 22; without them: one merged body, 12 SALU but
+    every axis's copies); its trace loop at most 150 SALU (124; without: 205)."""
     _, body = _kernel(isa, "ILj4ELi2ELb0E")
     loops = _loops(body)
     quad = [(h, c) for h, d, c in loops if d == 3 and c["v_or3_b32"] > 0 and any(k.startswith("s_load") for k in c)]
     assert len(quad) == 1, [(h, d) for h, d, _ in loops]
     _, c = quad[0]
-    assert c["v_or3_b32"] == 7, ("per-axis QUADAA bodies merged", c["v_or3_b32"])
+    assert c["v_or3_b32"] == 6, ("per-axis QUADAA bodies merged", c["v_or3_b32"])
     assert c["s_and_saveexec_b64"] == 0, c["s_and_saveexec_b64"]
-    assert _salu(c) <= 32, _salu(c)
+    assert _salu(c) <= 28, _salu(c)
     trace = [c for h, d, c in loops if d == 2 and _salu(c) > 60]
     assert len(trace) == 1 and _salu(trace[0]) <= 150, [_salu(c) for c in trace]
 
