@@ -52,7 +52,8 @@ constexpr int kBlock = 256;
 #define RT2_EXP_TWICE 0  // cost probes (bits): 1 resolve_hit, 2 rand_unit_vec3, 4 camera_ray, 8 slab test,
                          // 16 quad-run test, 32 threaded medium step, 64 its log, 128 its two boundary
                          // queries, 256 a Philox block (at every refill), 512 the sample store /
-                         // staging, 2048 a threaded transform entry (ray into model space, its reciprocal)
+                         // staging, 2048 a threaded transform entry (ray into model space, its reciprocal),
+                         // 4096 an accelerated list's lane walk
 #endif
 #ifndef RT2_EXP_WAVESTEPS
 #define RT2_EXP_WAVESTEPS 0  // diagnostic build: per-wave linear-traversal step counts into diag slots
@@ -1721,6 +1722,40 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
         // eight copies of the tree (compile.cpp): the one ordered nearer-first for this ray's octant
         if (end - j > st.w) j += st.w * ((d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u));
         const uint32_t stop = j + st.w;
+#if RT2_EXP_TWICE & 4096
+        {  // cost probe: the same walk on copies of the lane's state, result discarded
+          f3 o2 = o;
+          asm volatile("" : "+v"(o2.x), "+v"(o2.y), "+v"(o2.z));
+          float tmax2 = tmax;
+          uint32_t prim2 = prim, best2 = acc_best, j2 = j;
+          while (j2 < stop) {
+            const uint4 e0 = wide[4u * j2], e1 = wide[4u * j2 + 1u], e2 = wide[4u * j2 + 2u], e3 = wide[4u * j2 + 3u];
+            if (e0.x == kAccBvh) {
+              const bool in = acc_slab(mk(uf(e1.x), uf(e1.y), uf(e1.z)), mk(uf(e2.x), uf(e2.y), uf(e2.z)), o2, inv,
+                                       acc_pinv, tmin, tmax2);
+              uint32_t nx = in ? j2 + 1u : e0.y;
+              if (e0.z != j2 + 1u) {
+                const bool in2 = acc_slab(mk(uf(e1.w), uf(e2.w), uf(e3.x)), mk(uf(e3.y), uf(e3.z), uf(e3.w)), o2, inv,
+                                          acc_pinv, tmin, tmax2);
+                nx = in ? (in2 ? e0.z : e0.w) : e0.y;
+              }
+              j2 = nx;
+            } else {
+              float t;
+              if (sphere_t_rec<0, Has<F, kFeatMotion>()>(make_float4(uf(e1.x), uf(e1.y), uf(e1.z), uf(e1.w)),
+                                                         make_float4(uf(e2.x), uf(e2.y), uf(e2.z), uf(e2.w)), o2, d,
+                                                         time, tmin, FLT_MAX, t) &&
+                  (t < tmax2 || (t == tmax2 && best2 != kRefNone && e0.w < best2))) {
+                tmax2 = t;
+                prim2 = make_ref(kSphere, e0.z);
+                best2 = e0.w;
+              }
+              j2++;
+            }
+          }
+          asm volatile("" ::"v"(tmax2), "v"(prim2), "v"(best2));
+        }
+#endif
         while (j < stop) {
           // e0 = (kind, skip, after a hit, after a paired miss), e1..e3 = words 4..15
           const uint4 e0 = wide[4u * j], e1 = wide[4u * j + 1u], e2 = wide[4u * j + 2u], e3 = wide[4u * j + 3u];
