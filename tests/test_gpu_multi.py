@@ -6,8 +6,9 @@ On the one-GPU test box:
   * a device listed n times runs n row-band partitions on one GPU with device-local copies in
     place of RCCL: the partition, padding, de-interleave and Pixels() logic of an n-GPU job;
   * rt2_tracer_join with world 1 runs the one-process-per-GPU path (ncclCommInitRank).
-The multi-process RCCL path at N > 1 is exercised by bench.py under torch.distributed.run; its
-partition/gather glue is covered on CPU by tests/test_dist.py.
+The multi-process path (bench.py under torch.distributed.run) runs in tests/test_gpu_bench.py at world 1
+over RCCL and at world 2 with both ranks on GPU 0 over gloo; its partition/gather glue is covered on CPU
+by tests/test_dist.py.
 """
 import numpy as np
 import pytest
