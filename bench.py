@@ -20,9 +20,10 @@ Multi-GPU goes through the C ABI (include/rt2.h), not torch:
     split (all: every rank in turn); no gather.
 
 Rank 0 prints one JSON line (contract in the task statement) with a `roofline` object for the render
-kernel (bound: VALU or scalar issue; PMC instruction density from a committed profile of this kernel build and
-config x the live rays / HIP-event launch time) and a `cpu_baseline` object (the oracle restatement
-on every host core this process may use, bounded sample).
+kernel (frac: SURVEY §8(d)'s useful fp32 flops per ray x the live rays / the launches' own GPU time, over
+the fp32 vector peak; the VALU and scalar issue fractions from a committed PMC profile of this kernel
+build and config as named companions) and a `cpu_baseline` object (the oracle restatement on every
+host core this process may use, bounded sample).
 """
 import argparse
 import glob
@@ -87,7 +88,7 @@ def parse():
     ap.add_argument("--work-split", type=int, default=-1,
                     help="work items (pixel x frame chunk) per resident lane (-1: library default, 0: no split)")
     ap.add_argument("--batch-max", type=int, default=0, help="work items a wave reserves at once (0: default)")
-    ap.add_argument("--sample-budget-gb", type=float, default=0.0, help="per-frame sample buffer bound (0: default)")
+    ap.add_argument("--sample-budget-gb", type=float, default=0.0, help="bound on both launch slots' per-frame sample buffers together, GiB (0: default 24)")
     ap.add_argument("--plain", action="store_true", help="one GPU, no gather (the one-GPU tracer alone)")
     ap.add_argument("--emulate-world", type=int, default=1,
                     help="diagnostic: render one rank's row bands of an N-GPU split on this one GPU (no gather)")
@@ -149,16 +150,20 @@ def find_profile(key):
 
 
 def roofline_for(tr, rays_local, launches, kernel_ms, key, rank_stats_frames, spp_total, steps, ms_per_step):
-    """Roofline of the render kernel on this GPU: the kernel is issue bound (DESIGN.md §4 Roofline),
-    on the vector pipe (VALU lane-operations per second = the VALU instructions per ray of the
-    matching PMC profile x 64 x this run's rays per launch / this run's launch time) or on
-    the CU's one scalar unit (SALU instructions per second, same scaling); `bound` is the pipe with
-    the larger fraction of its peak, and both fractions are reported (valu_frac, salu_frac).
-    Also: the HBM fraction (profile traffic per ray, same scaling), the §8(d) useful-flop fraction
-    and the scene-record rate (bytes of records touched per ray / launch time, not an HBM figure).
-    Launch time = the render kernel's GPU time per launch (rt2_stats.kernel_ms: each launch timed by
-    its own clock from its first wave to its last, overlapping launches counted once). A kernel time
-    per step above the step's wall time would be a timing fault: then no fraction is reported."""
+    """Roofline of the render kernel on this GPU, as SURVEY.md §8(d) defines it.
+
+    `frac` is §8(d)'s useful-flop fraction: rays/s x F_ray / the FP32 vector peak (157.3 TFLOP/s), with
+    F_ray = the records each ray touched (counted by the kernel's counting pass at this run's seed) x the
+    per-test flop constants (AABB 18, quad 45, sphere 30, transform 45, medium 20). The kernel is issue
+    bound (DESIGN.md §4 Roofline), so the named companions say where the rest of the issue goes:
+    `valu_issue_frac` (VALU wave instructions per ray of the matching PMC profile x 64 lanes x rays per
+    launch / launch time / 78.6 T lane-op/s, masked lanes included) and `salu_frac` (the CU's one scalar
+    unit, 614 G instructions/s). §8(d)'s HBM model (records x record bytes per ray) is reported as
+    `record_rate_over_hbm_peak`: those records are scalar-cache hits on a few-KB scene program, so it is
+    not a physical HBM fraction; `hbm_frac` is the PMC-measured one (profile traffic per ray, same scaling).
+    Launch time = the render kernel's GPU time per launch (rt2_stats.kernel_ms: each launch timed by its
+    own clock from its first wave to its last, overlapping launches counted once). A kernel time per step
+    above the step's wall time would be a timing fault: then no fraction is reported."""
     tr.enable_stats(True)
     tr.Reset()
     tr.reset_stats()
@@ -171,39 +176,42 @@ def roofline_for(tr, rays_local, launches, kernel_ms, key, rank_stats_frames, sp
     rays_per_launch = rays_local / max(1, launches)
     avg_launch_s = kernel_ms / 1e3 / max(1, launches)
     src, prof, stale = find_profile(key)
-    out = {"bound": "valu_issue", "unit": "Tlane-op/s", "peak": round(VALU_PEAK_TLANE_OPS, 2),
+    out = {"bound": "valu", "model": "SURVEY §8(d) useful fp32 flops per ray x rays/s over the fp32 vector peak",
+           "unit": "TFLOP/s", "peak": FP32_VALU_PEAK_TFLOPS,
            "achieved": None, "frac": None, "traffic": None, "traffic_unit": "HBM bytes per launch (PMC)",
            "kernel": "rt2::dev::render_kernel<..., false>", "avg_launch_ms": round(avg_launch_s * 1e3, 3),
-           "rays_per_launch": int(rays_per_launch), "profile": src, "profile_stale": stale,
-           "kernel_ms_per_step": round(kernel_ms / max(1, steps), 2)}
+           "rays_per_launch": int(rays_per_launch), "flops_per_ray": round(f_ray, 1), "profile": src,
+           "profile_stale": stale, "kernel_ms_per_step": round(kernel_ms / max(1, steps), 2)}
     consistent = kernel_ms / max(1, steps) <= ms_per_step * 1.001
     if not consistent:
         out["invalid"] = (f"kernel time per step {kernel_ms / max(1, steps):.2f} ms exceeds the step's wall time "
                           f"{ms_per_step:.2f} ms: no fraction reported")
-    if prof and consistent:
+        return out
+    useful = rays_per_launch * f_ray / avg_launch_s / 1e12
+    out.update(achieved=round(useful, 3), frac=round(useful / FP32_VALU_PEAK_TFLOPS, 4))
+    out["useful_flop_frac"] = out["frac"]
+    if prof:
         pr = prof["per_ray"]
         valu = pr["valu_insts"] * rays_per_launch  # wave instructions per launch
         salu = pr.get("salu_insts", 0.0) * rays_per_launch
         valu_rate = valu * 64 / avg_launch_s / 1e12
         salu_rate = salu / avg_launch_s / 1e9
-        out["valu_frac"] = round(valu_rate / VALU_PEAK_TLANE_OPS, 4)
+        out["valu_issue_frac"] = round(valu_rate / VALU_PEAK_TLANE_OPS, 4)
+        out["valu_issue_tlane_ops"] = round(valu_rate, 3)
+        out["valu_issue_peak"] = round(VALU_PEAK_TLANE_OPS, 2)
         out["salu_frac"] = round(salu_rate / SALU_PEAK_GINST, 4)
-        if out["salu_frac"] > out["valu_frac"]:
-            out.update(bound="salu_issue", unit="Ginst/s", peak=round(SALU_PEAK_GINST, 1),
-                       achieved=round(salu_rate, 2), frac=out["salu_frac"])
-        else:
-            out.update(achieved=round(valu_rate, 3), frac=out["valu_frac"])
         out["valu_insts_per_ray"] = round(pr["valu_insts"], 3)
         out["salu_insts_per_ray"] = round(pr.get("salu_insts", 0.0), 3)
+        # issued lane slots per useful flop (masked lanes, traversal bookkeeping, exact-division sequences)
+        out["issued_lane_slots_per_useful_flop"] = round(pr["valu_insts"] * 64 / max(1e-9, f_ray), 3)
         if pr.get("hbm_bytes") is not None:
             out["traffic"] = int(pr["hbm_bytes"] * rays_per_launch)
             out["hbm_frac"] = round(out["traffic"] / avg_launch_s / 1e9 / HBM_PEAK_GBS, 4)
         out["profile_kernel_sha"] = (prof.get("key") or {}).get("kernel_sha")
-    if not consistent:
-        return out
-    out["useful_flop_frac"] = round(rays_per_launch * f_ray / avg_launch_s / 1e12 / FP32_VALU_PEAK_TFLOPS, 4)
     frame_bytes = 12 * spp_total  # the float3 sample store per (pixel, frame), per launch below
     out["record_rate_gbs"] = round((rays_per_launch * b_ray) / avg_launch_s / 1e9, 1)
+    out["record_rate_over_hbm_peak"] = round(out["record_rate_gbs"] / HBM_PEAK_GBS, 3)
+    out["record_rate_note"] = "§8(d) HBM model; the records are scalar-cache hits, not HBM traffic (see hbm_frac)"
     out["record_bytes_per_ray"] = round(b_ray, 1)
     out["records_per_ray"] = {k: round(v, 3) for k, v in per_ray.items()}
     out["sample_store_bytes_per_launch"] = frame_bytes
@@ -366,6 +374,8 @@ def main():
                          "gather_ms": st["gather_ms"],
                          "gathers": st["gathers"], "enqueue_ms": st.get("enqueue_ms", 0.0),
                          "readbacks": st.get("readbacks", 0), "readback_ms": st.get("readback_ms", 0.0),
+                         "sample_buffer_bytes": st.get("sample_buffer_bytes", 0),
+                         "device_bytes_peak": st.get("device_bytes_peak", 0),
                          "mray_s": st["rays"] / el / 1e6})
         if mode == "multi" and new_abi:  # each GPU of the one-process tracer
             per_rank[-1]["gpus"] = []
@@ -491,6 +501,10 @@ def main():
                        "readback_ms_per_step": round(per_rank[0]["readback_ms"] / a.steps, 3),
                        "readback_bytes_per_step": (a.width * a.height * 12 if per_rank[0]["readbacks"] else 0),
                        "enqueue_ms_per_step": round(per_rank[0]["enqueue_ms"] / a.steps, 3),
+                       # device memory per GPU: both launch slots' sample buffers (bounded by the total
+                       # sample budget, rt2.h) and the high-water mark of everything the tracer holds
+                       "sample_buffer_bytes": max(r.get("sample_buffer_bytes", 0) for r in per_rank),
+                       "device_bytes_peak_per_gpu": max(r.get("device_bytes_peak", 0) for r in per_rank),
                        "per_rank": [{"rank": r["rank"], "rows": r["rows"], "mray_s": round(r["mray_s"], 1),
                                      "ms_per_step": round(r["elapsed_s"] * 1e3 / a.steps, 2),
                                      "kernel_ms_per_step": round(r["kernel_ms"] / a.steps, 2)} for r in per_rank],

@@ -116,11 +116,11 @@ RT2_API int rt2_tracer_set_launch_frames(rt2_tracer* tr, int frames_per_launch);
  * `items_per_lane` (default 16), at least 1 and at most 64 (RT2_CHUNK_MAX): long items early, short
  * ones at the end of the launch. 0 = one chunk (each pixel's frames in one item). Every frame's
  * sample goes to a per-frame buffer and is summed in frame order after the launch, so results do
- * not depend on the split. The buffer is bounded by `bytes` (default 16 GiB): a render needing
- * more runs as several launches. The bound applies to each of the tracer's two launch slots
- * (consecutive launches alternate between two sample buffers so that a launch's tail overlaps the
- * next launch): the device memory the samples may take is 2 x `bytes` (32 GiB by default, of the
- * MI355X's 288 GB), per GPU. */
+ * not depend on the split. `bytes` bounds the device memory the samples take on each GPU in total
+ * (default 24 GiB of the MI355X's 288 GB): consecutive launches alternate between two launch slots,
+ * each with its own sample buffer of at most bytes / 2, so that a launch's tail overlaps the next
+ * launch; a render needing more than bytes / 2 of samples runs as several launches (at least one
+ * 8-frame octet each). rt2_stats.sample_buffer_bytes / device_bytes_peak report what is held. */
 RT2_API int rt2_tracer_set_lazy_frames(rt2_tracer* tr, int max_queued);
 RT2_API int rt2_tracer_flush(rt2_tracer* tr); /* launch the queued frames now (does not wait) */
 RT2_API int rt2_tracer_set_work_split(rt2_tracer* tr, int items_per_lane);
@@ -256,6 +256,11 @@ typedef struct {
   /* the sum of the render launches' first-wave-to-last-wave times (>= kernel_ms: overlaps counted
    * once per launch) */
   double launch_ms_sum;
+  /* device memory: both launch slots' per-frame sample buffers now (<= the sample budget), and the
+   * high-water mark of everything this tracer holds on its GPU (scene program, frame buffers, sample
+   * buffers, chunk tables, a root's gathered image). A multi-GPU tracer: the largest GPU's. */
+  uint64_t sample_buffer_bytes;
+  uint64_t device_bytes_peak;
 } rt2_stats;
 RT2_API int rt2_tracer_get_stats(rt2_tracer* tr, rt2_stats* out);
 /* The stats of GPU `part` of a multi-GPU tracer (part 0 of a one-GPU tracer is itself). */

@@ -63,7 +63,9 @@ class Stats(ctypes.Structure):
                                                                            ("readbacks", ctypes.c_uint64),
                                                                            ("readback_ms", ctypes.c_double),
                                                                            ("host_waits", ctypes.c_uint64),
-                                                                           ("launch_ms_sum", ctypes.c_double)]
+                                                                           ("launch_ms_sum", ctypes.c_double),
+                                                                           ("sample_buffer_bytes", ctypes.c_uint64),
+                                                                           ("device_bytes_peak", ctypes.c_uint64)]
 
     def as_dict(self):
         d = {n: (getattr(self, n) if n.endswith("_ms") else int(getattr(self, n))) for n, _ in self._fields_

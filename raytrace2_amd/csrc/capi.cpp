@@ -38,6 +38,12 @@ hipError_t LaunchDeinterleave(const float* stacks, float* image, float* image_nc
 
 using namespace rt2;
 
+// Default bound on the per-frame sample buffers of both launch slots together (rt2.h
+// rt2_tracer_set_sample_budget). Each slot gets half, so a 1024^2 image runs 1000 frames (11.7 GiB of
+// samples) in one launch per slot: the headline renders one launch per step. Measured on the final
+// round-6 kernel, one MI355X: DESIGN.md §3 "Sample buffer budget".
+constexpr size_t kDefaultSampleBudget = size_t(24) << 30;
+
 struct rt2_scene {
   Scene scene;
   CompiledScene compiled;
@@ -111,7 +117,11 @@ struct rt2_tracer {
   Slot slots[2];
   int next_slot = 0;
   bool pipeline = true;  // RT2_PIPELINE=0: every launch waits for the tracer stream (no overlap)
-  size_t sample_budget = size_t(16) << 30;  // bytes; bounds the frames per launch
+  // bytes: the bound on both launch slots' sample buffers together (each slot gets half; a render
+  // needing more runs as several launches, rt2.h rt2_tracer_set_sample_budget)
+  size_t sample_budget = kDefaultSampleBudget;
+  size_t scene_bytes = 0;         // scene program, tables and small per-tracer buffers on the device
+  size_t device_bytes_peak = 0;   // high-water mark of DeviceBytes()
   int work_split = 16;                     // chunk schedule: work left split into >= k items per lane (0: one chunk)
   int chunk_max = 64;                      // longest chunk (frames)
   int frame_tiles_env = -1;                // RT2_FRAME_TILES: -1 auto, 0 off, 1 on
@@ -245,6 +255,17 @@ void FreeFrame(rt2_tracer* t) {
   FreeImage(t);
 }
 
+// Device bytes this tracer holds now: the scene program and small buffers, the frame buffers, both
+// launch slots' sample buffers and chunk tables, and a root's gathered image.
+size_t DeviceBytes(const rt2_tracer* t) {
+  const size_t n = (size_t)t->width * (size_t)AllocRows(t);
+  size_t b = t->scene_bytes + (t->d_accum ? n * 12 : 0) + (t->d_pixels ? n * 4 : 0) + (t->d_ray_counts ? n * 4 : 0);
+  for (const auto& sl : t->slots) b += sl.samples_bytes + sl.chunks_bytes;
+  if (t->d_image) b += t->stacks_bytes + t->image_pixels * (12 + 12 + 4);
+  return b;
+}
+void NoteDeviceBytes(rt2_tracer* t) { t->device_bytes_peak = std::max(t->device_bytes_peak, DeviceBytes(t)); }
+
 int Realloc(rt2_tracer* t) {
   FreeFrame(t);
   t->local_rows = t->height > 0 ? LocalRows(t->height, BandH(t), t->rank, t->world) : 0;
@@ -253,6 +274,7 @@ int Realloc(rt2_tracer* t) {
   HIP_TRY(hipMalloc(&t->d_accum, n * 3 * sizeof(float)));
   HIP_TRY(hipMalloc(&t->d_pixels, n * 4));
   if (t->ray_counts_on) HIP_TRY(hipMalloc(&t->d_ray_counts, n * sizeof(uint32_t)));
+  NoteDeviceBytes(t);
   return RT2_OK;
 }
 
@@ -590,6 +612,11 @@ int rt2_tracer_create(const rt2_scene* s, int device, rt2_tracer** out) {
   }
   HIP_TRY(hipMalloc(&t->d_stats, kStatsSlots * sizeof(unsigned long long)));
   HIP_TRY(hipMemset(t->d_stats, 0, kStatsSlots * sizeof(unsigned long long)));
+  t->scene_bytes = c.nodes.size() * sizeof(float) + std::max<size_t>(mats.size(), 8) * sizeof(float) +
+                   c.textures.size() * sizeof(float) + c.perlin_vec.size() * sizeof(float) +
+                   c.perlin_perm.size() * sizeof(int) + c.lin.size() * sizeof(uint32_t) +
+                   c.lin_wide.size() * sizeof(uint32_t) + c.lind.size() * sizeof(float) + 128 +
+                   2 * sizeof(unsigned long long) * kClockRing + kStatsSlots * sizeof(unsigned long long);
   t->root = c.root;
   t->node_records = (uint32_t)(c.nodes.size() / 4);
   t->hot_records = c.hot_records;
@@ -1091,8 +1118,9 @@ int LaunchFrames(rt2_tracer* t, int n_frames) {
   // frames per launch: the caller's launch_frames, bounded by the sample-buffer budget
   const size_t frame_bytes = (size_t)p.local_pixels * 3 * sizeof(float);
   int per_launch = t->launch_frames > 0 ? std::min(t->launch_frames, n_frames) : n_frames;
-  // (the buffer holds whole octets of frames, rt2_layout.h kOctet)
-  const size_t budget_frames = std::max<size_t>(1, t->sample_budget / frame_bytes);
+  // (the buffer holds whole octets of frames, rt2_layout.h kOctet; each of the two slots gets half the
+  // budget, so both together stay within it)
+  const size_t budget_frames = std::max<size_t>(1, t->sample_budget / 2 / frame_bytes);
   per_launch = (int)std::min<size_t>((size_t)per_launch, budget_frames < kOctet ? budget_frames : budget_frames - budget_frames % kOctet);
   if (t->frame_tiles) {  // items (64-frame groups x 64 x local pixels) stay below 2^31
     const size_t groups = std::max<size_t>(1, (size_t)0x7FFFFFFF / (64u * (size_t)p.local_pixels));
@@ -1147,6 +1175,7 @@ int LaunchFrames(rt2_tracer* t, int n_frames) {
       sl.samples_bytes = 0;
       HIP_TRY(hipMallocAsync((void**)&sl.samples, need, sl.stream));
       sl.samples_bytes = need;
+      NoteDeviceBytes(t);
     }
     p.samples = sl.samples;
     const std::vector<uint32_t> tab(tabs.begin() + (long)L.table, tabs.begin() + (long)L.table + 2 * (L.n_chunks + 1));
@@ -1223,6 +1252,7 @@ int EnsureImage(rt2_tracer* root) {
   HIP_TRY(hipMalloc(&root->d_image_px, std::max<size_t>(npix * 4, 4)));
   root->stacks_bytes = stacks;
   root->image_pixels = npix;
+  NoteDeviceBytes(root);
   return RT2_OK;
 }
 
@@ -1576,6 +1606,8 @@ int rt2_tracer_get_stats(rt2_tracer* t, rt2_stats* o) {
       sum.readbacks += s.readbacks;
       sum.readback_ms += s.readback_ms;
       sum.host_waits += s.host_waits;
+      sum.sample_buffer_bytes = std::max(sum.sample_buffer_bytes, s.sample_buffer_bytes);
+      sum.device_bytes_peak = std::max(sum.device_bytes_peak, s.device_bytes_peak);
     }
     *o = sum;
     return RT2_OK;
@@ -1607,6 +1639,8 @@ int rt2_tracer_get_stats(rt2_tracer* t, rt2_stats* o) {
   o->readbacks = t->readbacks;
   o->readback_ms = t->readback_ms;
   o->host_waits = t->host_waits;
+  o->sample_buffer_bytes = t->slots[0].samples_bytes + t->slots[1].samples_bytes;
+  o->device_bytes_peak = std::max(t->device_bytes_peak, DeviceBytes(t));
   return RT2_OK;
 }
 

@@ -132,27 +132,28 @@ def _band_frame_bytes(w, h, band_h, rank, world):
     return w * rows * 12
 
 
-@pytest.mark.parametrize("boundary,how", [(2000, "launch_frames"), (2232, "sample_budget")])
+@pytest.mark.parametrize("boundary,how", [(2000, "launch_frames"), (1672, "sample_budget")])
 def test_c5_book2_across_a_launch_boundary(boundary, how):
-    """Book 2 (C5: 800x800 @ 10000 spp, frame tiles) across a launch boundary: the bench's 16 GiB
-    sample budget cuts its render into launches of 2232 frames (budget_frames rounded to octets);
-    frames boundary-10 .. boundary+10 on a full-width band are continued by the oracle from the GPU's
-    accumulation and must match bit for bit (RayTracer.cpp:55-70 renders every frame alike)."""
+    """Book 2 (C5: 800x800 @ 10000 spp, frame tiles) across a launch boundary: the default 24 GiB
+    sample budget (12 GiB per launch slot) cuts its one-GPU render into launches of 1672 frames
+    (budget_frames rounded to octets); frames boundary-10 .. boundary+10 on a full-width band are
+    continued by the oracle from the GPU's accumulation and must match bit for bit
+    (RayTracer.cpp:55-70 renders every frame alike)."""
     part = dict(band_h=8, rank=50, world=100)
     launch = ({"launch_frames": boundary} if how == "launch_frames" else
-              {"sample_budget": boundary * _band_frame_bytes(800, 800, **part)})
+              {"sample_budget": 2 * boundary * _band_frame_bytes(800, 800, **part)})
     st = _check_continuation("book2_final_scene_10000_samples", 800, 800, 10000, boundary - 10, boundary + 10,
                              launch=launch, **part)
     assert st["launches"] == 2
 
 
-@pytest.mark.parametrize("boundary,how", [(1333, "launch_frames"), (1360, "sample_budget")])
+@pytest.mark.parametrize("boundary,how", [(1333, "launch_frames"), (1024, "sample_budget")])
 def test_c4_cornell_volume_across_a_launch_boundary(boundary, how):
-    """Cornell volume (C4: 1024^2 @ 4000 spp) across the bench's launch boundary (16 GiB budget:
-    launches of 1360 frames) and an odd one (1333, launch_frames), continued by the oracle."""
+    """Cornell volume (C4: 1024^2 @ 4000 spp) across the bench's launch boundary (24 GiB budget, 12 GiB
+    per slot: launches of 1024 frames) and an odd one (1333, launch_frames), continued by the oracle."""
     part = dict(band_h=8, rank=40, world=128)
     launch = ({"launch_frames": boundary} if how == "launch_frames" else
-              {"sample_budget": boundary * _band_frame_bytes(1024, 1024, **part)})
+              {"sample_budget": 2 * boundary * _band_frame_bytes(1024, 1024, **part)})
     st = _check_continuation("cornell_box_volume", 1024, 1024, 4000, boundary - 10, boundary + 10, launch=launch,
                              **part)
     assert st["launches"] == 2

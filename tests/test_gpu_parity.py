@@ -83,8 +83,8 @@ def test_work_split_is_invisible(have_gpu, name):
     assert np.array_equal(base[1], o_rc)
     frame_bytes = w * h * 12
     for kw in (dict(work_split=1), dict(work_split=100000), dict(work_split=64, batch_max=1),
-               dict(work_split=64, batch_max=4096), dict(sample_budget=3 * frame_bytes),
-               dict(sample_budget=1, work_split=5), dict(launch_frames=4, sample_budget=2 * frame_bytes)):
+               dict(work_split=64, batch_max=4096), dict(sample_budget=6 * frame_bytes),
+               dict(sample_budget=1, work_split=5), dict(launch_frames=4, sample_budget=4 * frame_bytes)):
         acc, rc, st, px = gpu_render(name, w, h, spp, frames, **kw)
         assert np.array_equal(acc.view(np.uint32), base[0].view(np.uint32)), kw
         assert np.array_equal(rc, base[1]), kw

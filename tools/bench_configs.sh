@@ -11,7 +11,7 @@ run() {  # label, args...
   local rc=$?
   local line=$(grep '^{' gpurun_out/cfg.log)
   echo "{\"config\": \"$label\", \"args\": \"$*\", \"rc\": $rc, \"bench\": ${line:-null}}" >> gpurun_out/configs.jsonl
-  echo "[$label] rc=$rc $(echo "$line" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline'] or {}; print(d['value'], d['ms_per_step'], r.get('frac'), r.get('hbm_frac'), r.get('profile'))" 2>/dev/null)"
+  echo "[$label] rc=$rc $(echo "$line" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline'] or {}; print(d['value'], d['ms_per_step'], r.get('frac'), r.get('valu_issue_frac'), r.get('hbm_frac'), r.get('profile'))" 2>/dev/null)"
   case $rc in 0) ;; *) tail -5 gpurun_out/cfg.log; exit $rc;; esac
 }
 B1="--scene final_render_book_1.json --width 1920 --height 1080 --spp 500"

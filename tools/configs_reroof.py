@@ -26,8 +26,10 @@ for line in open(path):
         if prof and not stale:
             pr = prof["per_ray"]
             launch_s = r["avg_launch_ms"] / 1e3
-            r["achieved"] = round(pr["valu_insts"] * r["rays_per_launch"] * 64 / launch_s / 1e12, 3)
-            r["frac"] = round(r["achieved"] / VALU_PEAK_TLANE_OPS, 4)
+            # (frac is §8(d)'s useful-flop fraction, computed live by the bench; only the profile's
+            # issue and traffic companions are filled in here)
+            r["valu_issue_tlane_ops"] = round(pr["valu_insts"] * r["rays_per_launch"] * 64 / launch_s / 1e12, 3)
+            r["valu_issue_frac"] = round(r["valu_issue_tlane_ops"] / VALU_PEAK_TLANE_OPS, 4)
             r["valu_insts_per_ray"] = round(pr["valu_insts"], 3)
             r["salu_insts_per_ray"] = round(pr.get("salu_insts", 0.0), 3)
             if pr.get("hbm_bytes") is not None:
@@ -35,6 +37,6 @@ for line in open(path):
                 r["hbm_frac"] = round(r["traffic"] / launch_s / 1e9 / HBM_PEAK_GBS, 4)
             r["profile"], r["profile_stale"], r["profile_kernel_sha"] = src, False, key["kernel_sha"]
             r["recomputed"] = "after the run, from the committed profile of the same kernel build"
-            print(f"{d['config']}: frac {r['frac']} from {src}")
+            print(f"{d['config']}: valu_issue_frac {r['valu_issue_frac']} from {src}")
     out.append(json.dumps(d))
 open(path, "w").write("\n".join(out) + "\n")
