@@ -56,10 +56,40 @@ def test_c1_cornell_400_at_64spp_full_image():
     _check("cornell_box_original", 400, 400, 64, 64)
 
 
+def _check_recursive_order(name, w, h, spp, frames, acc, **part):
+    """The north star's literal bar against the reference-shaped product order: the oracle's recursive
+    RayColor (`emit + att * RayColor(...)`, RayTracer.cpp:20-45) on the same band and frames. The GPU
+    multiplies the attenuations front to back, so the two differ only in the rounding of the product:
+    per-pixel RMSE of clamp(accum / spp, 0, 1) (linear, per channel: SURVEY §8(d)) < 1e-3, and the
+    largest relative difference of the accumulated sums < 1e-5 (both sides add non-negative samples
+    in the same frame order, RayTracer.cpp:64)."""
+    from helpers import rmse
+    r_acc, _, _ = oracle_render(name, w, h, spp, frames, forward=False, threads=THREADS, **part)
+    ga = np.clip(acc.astype(np.float64) / spp, 0.0, 1.0)
+    ra = np.clip(r_acc.astype(np.float64) / spp, 0.0, 1.0)
+    e = rmse(ga, ra)
+    nz = r_acc != 0
+    rel = float(np.max(np.abs(acc[nz].astype(np.float64) - r_acc[nz]) / np.abs(r_acc[nz].astype(np.float64))))
+    assert np.array_equal(acc == 0, r_acc == 0)
+    assert e < 1e-3, e
+    assert rel < 1e-5, rel
+    print(f"{name} {w}x{h} spp {spp}, {frames} frames {part}: RMSE vs the recursive order {e:.3g}, "
+          f"max relative difference {rel:.3g}")
+
+
 def test_c2_cornell_1024_all_1000_frames_band():
     """BASELINE configs[1] (the headline): 1024^2, spp 1000, every frame 0..999 (strata wrap at
-    961), on rank 5 of a 32-way 16-row band split (32 rows x 1024)."""
-    _check("cornell_box_original", 1024, 1024, 1000, 1000, band_h=16, rank=5, world=32)
+    961), on rank 5 of a 32-way 16-row band split (32 rows x 1024): bit-identical to the oracle's
+    front-to-back order, and within the north star's tolerance of its recursive (reference) order."""
+    part = dict(band_h=16, rank=5, world=32)
+    acc, _ = _check("cornell_box_original", 1024, 1024, 1000, 1000, **part)
+    _check_recursive_order("cornell_box_original", 1024, 1024, 1000, 1000, acc, **part)
+
+
+def test_c2_cornell_1024_whole_image_4_frames():
+    """The whole 1024^2 headline image (every row, every pixel), frames 0..3 of the spp-1000
+    stratification: bit-identical to the oracle, ray counts included (about 30 M rays)."""
+    _check("cornell_box_original", 1024, 1024, 1000, 4)
 
 
 def test_c3_book1_full_width_band_all_500_frames():
@@ -79,8 +109,12 @@ def test_c4_cornell_volume_spp4000_across_sq2():
 
 
 def test_c5_book2_full_width_band():
-    """BASELINE configs[4]: book 2 at 800x800, spp 10000 (sq 100), 24 frames on an 8-row band."""
-    _check("book2_final_scene_10000_samples", 800, 800, 10000, 24, band_h=8, rank=50, world=100)
+    """BASELINE configs[4]: book 2 at 800x800, spp 10000 (sq 100), 24 frames on an 8-row band:
+    bit-identical to the oracle's front-to-back order, and within the north star's tolerance of its
+    recursive (reference) order."""
+    part = dict(band_h=8, rank=50, world=100)
+    acc, _ = _check("book2_final_scene_10000_samples", 800, 800, 10000, 24, **part)
+    _check_recursive_order("book2_final_scene_10000_samples", 800, 800, 10000, 24, acc, **part)
 
 
 @pytest.mark.parametrize("band_h", [1, 2, 4])
