@@ -70,6 +70,7 @@ struct rt2_tracer {
   int max_stack = 1;
   bool stack_ok = true;  // the scene fits the stack traversal (else only the threaded program runs it)
   bool flat_xforms = true;  // no nested transforms in the threaded program (RenderParams::flat_xforms)
+  bool origins_bounded = false;  // CompiledScene::origins_bounded: launches check the camera's range
   bool use_lds = true;
   bool use_hybrid = true;   // stage only the BVH prefix in LDS when the scene is too large
   bool force_hybrid = false;  // tests: hybrid even when the whole scene would fit
@@ -430,6 +431,7 @@ int rt2_scene_get_info(const rt2_scene* s, rt2_scene_info* o) {
   o->acc_lists = c.acc_lists;
   o->acc_nodes = c.acc_nodes;
   o->linear_steps = (int)(c.lin.size() / 4);
+  o->origins_bounded = c.origins_bounded ? 1 : 0;
   return RT2_OK;
 }
 
@@ -624,6 +626,7 @@ int rt2_tracer_create(const rt2_scene* s, int device, rt2_tracer** out) {
   t->max_stack = c.max_stack;
   t->stack_ok = c.stack_ok;
   t->flat_xforms = c.lin_xform_depth <= 1;
+  t->origins_bounded = c.origins_bounded;
   Put3(t->background, s->scene.background);
   t->camera = s->scene.cam;
   HIP_TRY(hipDeviceGetAttribute(&t->cus, hipDeviceAttributeMultiprocessorCount, device));
@@ -888,7 +891,8 @@ constexpr uint32_t kFrameTileMinSteps = 256;  // threaded programs longer than t
 
 // Camera rays start within +-2^64 on every axis (center + the defocus disk's two half-axes): the
 // kernel's rectangle test (compile.cpp RectAAWords) is exact for ray origins within +-2^100, and a
-// scene the compiler gives that test lies within +-2^64 (Flattener::QuadAASpace).
+// scene the compiler gives that test lies within +-2^64 (Flattener::QuadAASpace). Checked only for
+// scenes whose threaded program holds such a test (CompiledScene::origins_bounded).
 bool CameraOriginsBounded(const CameraParams& c) {
   for (int k = 0; k < 3; k++)
     if (!(std::fabs((double)c.center[k]) + std::fabs((double)c.defocus_u[k]) + std::fabs((double)c.defocus_v[k]) <=
@@ -1019,7 +1023,7 @@ int LaunchFrames(rt2_tracer* t, int n_frames) {
   memcpy(p.background, t->background, sizeof(p.background));
   p.cam = t->camera.Params();  // RayTracer::Update → camera->Update() (RayTracer.cpp:56)
   if (p.cam.sqrt_spp <= 0) return Fail(RT2_ERR_INVALID, "samples_per_pixel gives sqrt_spp = 0");
-  if (!CameraOriginsBounded(p.cam)) return Fail(RT2_ERR_INVALID, kCameraRangeMsg);
+  if (t->origins_bounded && !CameraOriginsBounded(p.cam)) return Fail(RT2_ERR_INVALID, kCameraRangeMsg);
   p.width = t->width;
   p.height = t->height;
   p.local_rows = t->local_rows;
@@ -1366,7 +1370,7 @@ int rt2_tracer_render(rt2_tracer* t, int n_frames) {
   if ((int64_t)t->frame_idx + t->queued + n_frames > 0x7FFFFFFF)
     return Fail(RT2_ERR_INVALID, "frame index overflow");
   if (t->camera.Params().sqrt_spp <= 0) return Fail(RT2_ERR_INVALID, "samples_per_pixel gives sqrt_spp = 0");
-  if (!CameraOriginsBounded(t->camera.Params())) return Fail(RT2_ERR_INVALID, kCameraRangeMsg);
+  if (t->origins_bounded && !CameraOriginsBounded(t->camera.Params())) return Fail(RT2_ERR_INVALID, kCameraRangeMsg);
   t->queued += n_frames;
   if (t->lazy_max > 0 && t->queued < t->lazy_max) return RT2_OK;
   return Flush(t);

@@ -135,6 +135,9 @@ void WorldNormal(const std::vector<float>& lind, uint32_t xf, const float n_mode
 }
 
 struct Flattener {
+  // the threaded program holds a test whose exactness needs ray origins within +-2^64 in world space
+  // (QUADAA rectangles, box boundaries as QUADAA words, transforms about y: CompiledScene::origins_bounded)
+  bool origins_bounded = false;
   const Scene& s;
   CompiledScene& out;
   std::unordered_map<int, uint32_t> ref_of;  // obj index -> node ref (DAG sharing)
@@ -504,6 +507,7 @@ struct Flattener {
       codes |= (axis - 4) << (3 * k);
     }
     lind.insert(lind.end(), words.begin(), words.end());
+    origins_bounded = true;
     return kBoundaryAAFlag | ((uint32_t)o.children.size() << 24) | codes;
   }
   // An accelerated list's tree in the threaded program: ACCBVH steps (padded box, skip = index
@@ -634,7 +638,9 @@ struct Flattener {
       case kXform: {
         uint32_t off = CopyRecords(src, kXformRecords, lind);
         lind[4 * (off + 1) + 3] = Bits(parent_xf);
-        lind[4 * (off + 2) + 3] = Bits(YAxisPattern(i, lind, off) ? kXformYAxis : 0u);
+        const bool yaxis = YAxisPattern(i, lind, off);
+        origins_bounded = origins_bounded || yaxis;
+        lind[4 * (off + 2) + 3] = Bits(yaxis ? kXformYAxis : 0u);
         uint32_t self = make_ref(kXform, off);
         if (xf_depth >= kLinearMaxXformDepth) return false;  // the kernel nests one loop per level
         size_t me = emit(kXform, off, 0);
@@ -667,6 +673,7 @@ struct Flattener {
         if (axis >= 4 && axis <= 6 && !(QuadAASpace(parent_xf, lind) && RectAAWords(r, (int)axis - 4, test))) axis -= 3;
         lind_axis[off] = axis;
         if (axis >= 4 && axis <= 6) {  // QUADAA layout (rt2_layout.h)
+          origins_bounded = true;
           const float n[3] = {r[0], r[1], r[2]}, d = r[3], q[3] = {r[4], r[5], r[6]}, mat = r[7];
           float w[3] = {q[0], q[1], q[2]};
           if (parent_xf != kRefNone) WorldNormal(lind, parent_xf, n, w);  // replaces q (unused here)
@@ -835,6 +842,7 @@ bool CompileSceneWith(const Scene& s, CompiledScene& out, std::string& err, bool
     out.lin.clear();
     out.lind.clear();
   }
+  out.origins_bounded = fl.origins_bounded && !out.lin.empty();
   // The stack traversal needs max_stack entries per lane; the threaded program needs none, so a
   // deeper scene still loads when it has one (and then always runs threaded).
   out.stack_ok = out.max_stack <= kTraversalStack;

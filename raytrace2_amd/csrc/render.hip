@@ -137,17 +137,26 @@ __device__ __forceinline__ f3 recip3(f3 d) {
     return mk(rcp_nr(d.x), rcp_nr(d.y), rcp_nr(d.z));
   return mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
 }
-// recip3 of a normalize result (every component is a NaN or has |x| <= 1 + 2^-21, so only the lower
-// end of rcp_nr's range needs a check; a NaN fails it), and whether the reciprocal is finite (on the
-// fast path by construction: |1 / x| <= 2^95)
-__device__ __forceinline__ void recip3_unit(f3 d, f3& inv, bool& fin) {
-  if (__all(fabsf(d.x) >= 0x1p-95f && fabsf(d.y) >= 0x1p-95f && fabsf(d.z) >= 0x1p-95f)) {
-    inv = mk(rcp_nr(d.x), rcp_nr(d.y), rcp_nr(d.z));
-    fin = true;
+// d = normalize(v), inv = (1/d.x, 1/d.y, 1/d.z) (IEEE) and whether inv is finite. When the whole wave
+// takes normalize's fast path (dot(v, v) in [2^-96, 2^126]), every component of d is a NaN or has
+// |x| <= 1 + 2^-21, so only the lower end of rcp_nr's range needs a check (a NaN fails it) and the
+// reciprocal is finite by construction (|1 / x| <= 2^95). normalize's slow path can give components of
+// any size (+-inf for a v so short that dot(v, v) underflows), and there the reciprocal is
+// IEEE division.
+__device__ __forceinline__ void normalize_recip3(f3 v, f3& d, f3& inv, bool& fin) {
+  const float l2 = dot(v, v);
+  if (__all(l2 >= 0x1p-96f && l2 <= 0x1p126f)) {
+    d = v * rcp_nr(sqrt_nr(l2));
+    if (__all(fabsf(d.x) >= 0x1p-95f && fabsf(d.y) >= 0x1p-95f && fabsf(d.z) >= 0x1p-95f)) {
+      inv = mk(rcp_nr(d.x), rcp_nr(d.y), rcp_nr(d.z));
+      fin = true;
+      return;
+    }
   } else {
-    inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    fin = __builtin_isfinite(inv.x) && __builtin_isfinite(inv.y) && __builtin_isfinite(inv.z);
+    d = v * (1.0f / sqrtf(l2));
   }
+  inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+  fin = __builtin_isfinite(inv.x) && __builtin_isfinite(inv.y) && __builtin_isfinite(inv.z);
 }
 __device__ __forceinline__ f3 xyz(float4 v) { return mk(v.x, v.y, v.z); }
 // floor(n / d) for n < 2^31 by the host's multiplier (rt2_layout.h Magic): v_mad_u64_u32 + shift
@@ -1644,8 +1653,7 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
                 uf(m[2]) * d.x + uf(m[6]) * d.y + uf(m[10]) * d.z);
       }
       o = no;
-      d = normalize(nd);
-      recip3_unit(d, inv, fin);
+      normalize_recip3(nd, d, inv, fin);
 #if RT2_EXP_TWICE & 2048
       {
         f3 o2 = o;
@@ -1662,10 +1670,9 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
           e2 = mk(uf(m[0]) * o2.x + uf(m[4]) * o2.y + uf(m[8]) * o2.z, uf(m[1]) * o2.x + uf(m[5]) * o2.y + uf(m[9]) * o2.z,
                   uf(m[2]) * o2.x + uf(m[6]) * o2.y + uf(m[10]) * o2.z);
         }
-        const f3 d2 = normalize(e2);
-        f3 i2;
+        f3 d2, i2;
         bool f2;
-        recip3_unit(d2, i2, f2);
+        normalize_recip3(e2, d2, i2, f2);
         asm volatile("" ::"v"(n2.x), "v"(n2.y), "v"(n2.z), "v"(i2.x), "v"(i2.y), "v"(i2.z), "v"((int)f2));
       }
 #endif

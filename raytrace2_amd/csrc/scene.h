@@ -147,6 +147,11 @@ struct CompiledScene {
   int acc_lists = 0, acc_nodes = 0;  // exact list acceleration trees (rt2_layout.h LISTACC)
   int bvh_depth = 0;
   uint32_t features = 0;          // rt2_layout.h Feature bits (defocus is added per render)
+  // The threaded program uses a test that is exact only for ray origins within +-2^64 in world space
+  // (QUADAA rectangles and box boundaries: compile.cpp RectAAWords; transforms about y: YAxisPattern):
+  // a launch then refuses a camera whose rays would start beyond that (capi.cpp CameraOriginsBounded).
+  // Scenes without such tests (e.g. spheres only) render any camera the reference does.
+  bool origins_bounded = false;
   std::vector<uint32_t> lin;      // threaded traversal program (4 words per step), empty if too long
   std::vector<float> lind;        // records of the program's steps, in program order (float4)
   std::vector<uint32_t> lin_wide; // 16 words per step: the lin entry + the first 12 words of its record,

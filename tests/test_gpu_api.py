@@ -55,6 +55,29 @@ def test_camera_beyond_the_exact_range_fails_loudly(tracer):
     assert tracer.FrameIdx() == 2 and np.isfinite(tracer.NonConvertedPixels()).all()
 
 
+def test_far_camera_renders_sphere_scenes_like_the_oracle():
+    """the +-2^64 camera bound belongs to the tests that need it (QUADAA rectangles, box
+    boundaries, transforms about y: CompiledScene::origins_bounded). A sphere-only scene renders a camera
+    beyond it as the reference would (here every ray misses: the sphere test's squares overflow), bit for
+    bit like the oracle."""
+    from oracle.oracle import OracleScene
+    name, w, h, spp, frames = "perlin_spheres", 24, 16, 4, 3
+    sc = R.Scene(scene_path(name), R.DEFAULT_SEED)
+    far = R.Camera((3e20, 2.0, 3.0), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 20.0, 0.0, 10.0)
+    tr = R.RayTracer(sc, 0)
+    tr.set_seed(R.DEFAULT_SEED)
+    tr.SetSamplesPerPixel(spp)
+    tr.OnResize((w, h))
+    tr.camera = far
+    tr.Render(frames)
+    acc = tr.Accumulation()
+    tr.close()
+    o = OracleScene(scene_path(name), R.DEFAULT_SEED)
+    o.set_camera(far.center, far.look_at, far.view_up, far.vfov, far.defocus_angle, far.focus_distance)
+    o_acc, _, _ = o.render(w, h, spp, frames, forward=True)
+    assert np.array_equal(acc.view(np.uint32), o_acc.view(np.uint32))
+
+
 def test_queued_frames_and_reset(tracer):
     for _ in range(5):
         tracer.Update()

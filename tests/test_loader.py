@@ -58,6 +58,15 @@ def test_scene_compile_facts():
     assert info.acc_lists == 0 and info.linear_steps > 0
 
 
+@pytest.mark.parametrize("name,bounded", [("cornell_box_original", 1), ("cornell_box_volume", 1),
+                                          ("book2_final_scene_10000_samples", 1), ("final_render_book_1", 0),
+                                          ("perlin_spheres", 0), ("checker_test", 0)])
+def test_camera_range_check_only_where_a_test_needs_it(name, bounded):
+    """only scenes whose threaded program holds a test exact for ray origins within +-2^64
+    (QUADAA rectangles, box boundaries, transforms about y) make a launch check the camera's range."""
+    assert R.Scene(scene_path(name)).info().origins_bounded == bounded
+
+
 def test_list_acceleration_can_be_disabled(monkeypatch):
     monkeypatch.setenv("RT2_NO_LIST_ACCEL", "1")
     b2 = R.Scene(scene_path("book2_final_scene_10000_samples")).info()
