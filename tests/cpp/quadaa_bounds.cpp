@@ -7,7 +7,8 @@
 // must equal Quad::Hit's interior test
 // (Quad.cpp:27-36: alpha = dot(w, cross(pv, v)), beta = dot(w, cross(u, pv)), pv = p - q, both in
 // [0, 1]) for hit points p around and on the bounds, at +-0, +-inf, NaN and far away, off the plane by
-// rounding (compile.cpp RectAAWords: corners and edges within +-2^40, ray origins within +-2^80). Prints the
+// rounding (compile.cpp RectAAWords: corners and edges within +-2^40, ray origins within +-2^100, so a hit
+// point lies off the plane by up to about 2^-20 (|q| + |o|) = 2^80). Prints the
 // number of decisions compared; exits non-zero at the first disagreement.
 #include <cfloat>
 #include <cmath>
@@ -45,10 +46,10 @@ int main(int argc, char** argv) {
   const int n = argc > 1 ? atoi(argv[1]) : 2000;
   std::mt19937_64 rng(argc > 2 ? strtoull(argv[2], nullptr, 10) : 1);
   std::uniform_real_distribution<float> unit(-1.0f, 1.0f);
-  auto magnitude = [&]() {  // 0, tiny, ordinary or huge, either sign
-    const int c = (int)(rng() % 8);
+  auto magnitude = [&]() {  // 0, tiny, ordinary, at the QUADAA limit (2^40) or huge, either sign
+    const int c = (int)(rng() % 9);
     if (c == 0) return 0.0f;
-    const float e = c == 1 ? -120.0f : (c == 2 ? 100.0f : (float)(rng() % 8) - 2.0f);
+    const float e = c == 1 ? -120.0f : (c == 2 ? 100.0f : (c == 3 ? 40.0f : (float)(rng() % 8) - 2.0f));
     return std::ldexp(unit(rng), (int)e);
   };
   long compared = 0;
@@ -101,8 +102,9 @@ int main(int argc, char** argv) {
         p[a] = ca[x];
         p[b] = cb[y];
         // the hit point's coordinate along the normal: on the plane up to the rounding of o + t d
-        // (a few ulps of the origin's and the corner's coordinates; origins within +-2^80)
-        const float off = std::ldexp(unit(rng), (int)(rng() % 100) - 20 - 24);
+        // (a few ulps of the origin's and the corner's coordinates; origins within +-2^100, so offsets
+        // up to 2^80: exponents -44 .. 80)
+        const float off = std::ldexp(unit(rng), (int)(rng() % 125) - 44);
         p[k] = (rng() & 3) == 0 ? q[k] : q[k] + off;
         const bool ref = reference_inside(p, q, u, v, w);
         const bool got = lo[0] <= p[a] && p[a] <= hi[0] && lo[1] <= p[b] && p[b] <= hi[1];
