@@ -259,10 +259,11 @@ inline void CosSin2Pi(float v, float& c, float& s) {
   const int q = (int)t;
   const float x = t - (float)q;
   const float x2 = x * x;
-  const float sp = ((((1.509560242993757e-4f * x2 + -4.672547802329063e-3f) * x2 + 7.968873530626297e-2f) * x2 +
-                     -6.459634304046631e-1f) * x2 + 1.570796251296997f) * x;
-  const float cp = (((8.59465915709734e-4f * x2 + -2.0813362672924995e-2f) * x2 + 2.536526620388031e-1f) * x2 +
-                    -1.2336987257003784f) * x2 + 1.0f;
+  // Horner steps as fused multiply-adds (one rounding each; the oracle evaluates the same fmas)
+  const float sp = std::fma(std::fma(std::fma(std::fma(1.509560242993757e-4f, x2, -4.672547802329063e-3f), x2, 7.968873530626297e-2f), x2,
+                             -6.459634304046631e-1f), x2, 1.570796251296997f) * x;
+  const float cp = std::fma(std::fma(std::fma(std::fma(8.59465915709734e-4f, x2, -2.0813362672924995e-2f), x2, 2.536526620388031e-1f), x2,
+                             -1.2336987257003784f), x2, 1.0f);
   switch (q) {
     case 0: c = cp; s = sp; break;
     case 1: c = -sp; s = cp; break;

@@ -649,10 +649,11 @@ __device__ __forceinline__ void cos_sin_2pi(float v, float& c, float& s) {
   const int q = (int)t;
   const float x = t - (float)q;
   const float x2 = x * x;
-  const float sp = ((((1.509560242993757e-4f * x2 + -4.672547802329063e-3f) * x2 + 7.968873530626297e-2f) * x2 +
-                     -6.459634304046631e-1f) * x2 + 1.570796251296997f) * x;
-  const float cp = (((8.59465915709734e-4f * x2 + -2.0813362672924995e-2f) * x2 + 2.536526620388031e-1f) * x2 +
-                    -1.2336987257003784f) * x2 + 1.0f;
+  // Horner steps as fused multiply-adds (one rounding each; the oracle evaluates the same fmas)
+  const float sp = fmaf(fmaf(fmaf(fmaf(1.509560242993757e-4f, x2, -4.672547802329063e-3f), x2, 7.968873530626297e-2f), x2,
+                             -6.459634304046631e-1f), x2, 1.570796251296997f) * x;
+  const float cp = fmaf(fmaf(fmaf(fmaf(8.59465915709734e-4f, x2, -2.0813362672924995e-2f), x2, 2.536526620388031e-1f), x2,
+                             -1.2336987257003784f), x2, 1.0f);
   const bool odd = (q & 1) != 0, neg_c = q == 1 || q == 2, neg_s = q >= 2;
   const float cc = odd ? sp : cp, ss = odd ? cp : sp;
   c = neg_c ? -cc : cc;
