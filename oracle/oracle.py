@@ -222,6 +222,14 @@ def log_u(v):
     return out
 
 
+def sin_f(v):
+    """SinF (the marble texture's sin of a float; shared with the kernel's sin_f)."""
+    v = np.ascontiguousarray(v, np.float32)
+    out = np.zeros(v.size, np.float32)
+    lib().oracle_samples(4, 0, 0, 0, v.size, _f(v), _f(out))
+    return out
+
+
 def quad_hit(q, u, v, o, d, tmin=0.001, tmax=3.4028234663852886e38):
     inp = np.array(list(q) + list(u) + list(v) + list(o) + list(d) + [tmin, tmax], np.float32)
     out = np.zeros(11, np.float32)

@@ -17,8 +17,8 @@
 //    thread_local std::minstd_rand seeded from std::random_device (Math.hpp:9-13).
 //  * Perlin tables are drawn from a Philox stream keyed by (seed, noise texture ordinal).
 //  * log() in ConstantMedium is the shared float polynomial LogU (within 1 ulp; the reference calls
-//    glibc logf, itself within an ulp); sin() in the marble texture is evaluated in double and
-//    rounded once (the reference calls sinf; difference <= 1 ulp).
+//    glibc logf, itself within an ulp); sin() in the marble texture is the shared float
+//    restatement SinF (within 9e-8 of sin for |x| <= 5000; the reference calls sinf).
 //  * pow(1-cos, 5) in Schlick is an explicit double multiplication chain (reference: std::pow).
 //  * RandUnitVec3 / RandInUnitDisk draw their (identical) distributions by inverse-CDF maps
 //    instead of rejection loops, with a shared polynomial sin/cos (see CosSin2Pi).
@@ -254,6 +254,25 @@ inline vec3 RandVec3(Rng& g, float min, float max) {
 // (cos 2 pi v, sin 2 pi v) for v in [0, 1): quarter turn by the exact split 4v = q + x, then
 // degree-9 odd / degree-8 even polynomials in x (max error 2e-7). The kernel evaluates the same
 // operations in the same order (render.hip cos_sin_2pi), so both round identically.
+// sin(x) of a float (the marble texture, Texture.cpp:16 std::sin): k = rint(x 2/pi), x - k pi/2 by a
+// three-part Cody-Waite split in fmas, quarter-turn polynomials in fmas; within 9e-8 of sin for
+// |x| <= 5000. |x| >= 2^24 gives x - x. The kernel's sin_f evaluates the same operations in the same
+// order (tests/test_oracle_kat.py pins it against sin).
+inline float SinF(float x) {
+  if (!(std::fabs(x) < 0x1p24f)) return x - x;
+  const float k = std::rint(x * 0.636619772f);
+  float r = std::fma(-k, 1.57079637f, x);
+  r = std::fma(-k, -4.37113883e-08f, r);
+  r = std::fma(-k, -1.71512451e-15f, r);
+  const float z = r * r;
+  const float s = std::fma(std::fma(std::fma(-1.9515295891e-4f, z, 8.3321608736e-3f), z, -1.6666654611e-1f), z * r, r);
+  const float c = std::fma(std::fma(std::fma(2.443315711809948e-5f, z, -1.388731625493765e-3f), z, 4.166664568298827e-2f),
+                           z * z, std::fma(-0.5f, z, 1.0f));
+  const int q = (int)(k - 4.0f * std::floor(k * 0.25f));
+  const float v = (q & 1) ? c : s;
+  return q >= 2 ? -v : v;
+}
+
 inline void CosSin2Pi(float v, float& c, float& s) {
   const float t = v * 4.0f;
   const int q = (int)t;
@@ -833,7 +852,7 @@ vec3 TexValue(const Scene& s, uint32_t idx, vec3 p) {
       if (t.noise_type == 1) {
         float arg = t.scale * p.z + 10 * t.perlin->Turb(p);
         if (g_controls & kCtlRefMath) return (t.albedo * 0.5f) * (1 + std::sin(arg));  // sinf (Texture.cpp:16)
-        return (t.albedo * 0.5f) * (1 + (float)std::sin((double)arg));
+        return (t.albedo * 0.5f) * (1 + SinF(arg));
       }
       return (t.albedo * 0.5f) * (1.0f + t.perlin->Noise(t.scale * p));
   }
@@ -1500,7 +1519,7 @@ void oracle_uniforms(uint64_t seed, uint32_t pixel, uint32_t frame, int n, float
 
 // n draws of RandUnitVec3 (which = 0) or RandInUnitDisk (which = 1) from the path stream of
 // (seed, pixel, frame), 3 floats each; which = 2: CosSin2Pi of the n uniforms in `in` (2 floats each);
-// which = 3: LogU of the n values in `in` (1 float each)
+// which = 3: LogU of the n values in `in` (1 float each); which = 4: SinF of them
 void oracle_samples(int which, uint64_t seed, uint32_t pixel, uint32_t frame, int n, const float* in, float* out) {
   Rng g(seed, pixel, frame, kTagPath);
   for (int i = 0; i < n; i++) {
@@ -1510,6 +1529,10 @@ void oracle_samples(int which, uint64_t seed, uint32_t pixel, uint32_t frame, in
     }
     if (which == 3) {
       out[i] = LogU(in[i]);
+      continue;
+    }
+    if (which == 4) {
+      out[i] = SinF(in[i]);
       continue;
     }
     vec3 v = which == 0 ? RandUnitVec3(g) : RandInUnitDisk(g);

@@ -659,6 +659,26 @@ __device__ __forceinline__ void cos_sin_2pi(float v, float& c, float& s) {
   c = neg_c ? -cc : cc;
   s = neg_s ? -ss : ss;
 }
+// sin(x) in float for the marble texture (Texture.cpp:16, std::sin of a float): x - k pi/2 with
+// k = rint(x 2/pi) by a three-part Cody-Waite split in fmas, then the quarter-turn polynomials of r in
+// [-pi/4, pi/4] (Horner steps as fmas); within 9e-8 of sin for |x| <= 5000 (the marble's arguments stay
+// below a few hundred). |x| >= 2^24 (no fractional part left) gives x - x: 0, or NaN for +-inf and NaN.
+// The oracle's SinF evaluates the same operations in the same order. (Round 5 took a double-precision
+// sin here, whose hoisted coefficients held 72 of book 2's 92 bytes of register-spill scratch.)
+__device__ __forceinline__ float sin_f(float x) {
+  if (!(fabsf(x) < 0x1p24f)) return x - x;
+  const float k = __builtin_rintf(x * 0.636619772f);
+  float r = fmaf(-k, 1.57079637f, x);
+  r = fmaf(-k, -4.37113883e-08f, r);
+  r = fmaf(-k, -1.71512451e-15f, r);
+  const float z = r * r;
+  const float s = fmaf(fmaf(fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f), z, -1.6666654611e-1f), z * r, r);
+  const float c = fmaf(fmaf(fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f), z, 4.166664568298827e-2f), z * z,
+                       fmaf(-0.5f, z, 1.0f));
+  const int q = (int)(k - 4.0f * floorf(k * 0.25f));  // k mod 4, exact for |k| < 2^25
+  const float v = (q & 1) ? c : s;
+  return q >= 2 ? -v : v;
+}
 // ln(u) of a 24-bit uniform (ConstantMedium.cpp:38 std::log(RandReal())): -inf at 0, else
 // e ln2 + log1p(f), u = 2^e (1 + f), 1 + f in [sqrt(1/2), sqrt(2)), log1p = f + f^2 Q(f) (degree-8 Q),
 // ln2 split so that e ln2_hi is exact; within 0.87 ulp of ln for every uniform. The oracle's LogU
@@ -1959,7 +1979,7 @@ __device__ __forceinline__ f3 tex_value(const ShadeArgs& S, uint32_t idx, f3 p) 
           tp = tp * 2.0f;
         }
         float arg = t1.x * p.z + 10.0f * fabsf(acc);
-        return alb * (1.0f + (float)sin((double)arg));
+        return alb * (1.0f + sin_f(arg));
       }
       return alb * (1.0f + perlin_noise(S, voff, poff, pc, t1.x * p));
     }

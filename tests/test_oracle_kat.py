@@ -158,6 +158,19 @@ def test_cos_sin_2pi_polynomial():
     assert cs[0, 0] == 1.0 and cs[0, 1] == 0.0
 
 
+def test_sin_f_restatement():
+    # the marble texture's sin (Texture.cpp:16; oracle SinF == kernel sin_f): within 9e-8 of sin over
+    # the marble's argument range and beyond, odd, exact at 0, 0 / NaN past 2^24
+    rng = np.random.default_rng(5)
+    v = np.concatenate([rng.uniform(-5000, 5000, 1 << 18), rng.uniform(-4, 4, 1 << 18),
+                        np.arange(-20000, 20000, dtype=np.float64) * (np.pi / 4)]).astype(np.float32)
+    s = O.sin_f(v).astype(np.float64)
+    assert np.abs(s - np.sin(v.astype(np.float64))).max() < 1e-7
+    assert np.array_equal(O.sin_f(-v), -O.sin_f(v))
+    sp = O.sin_f(np.array([0.0, -0.0, 2.0 ** 24, -(2.0 ** 30), np.inf, np.nan], np.float32))
+    assert sp[0] == 0 and sp[2] == 0 and sp[3] == 0 and np.isnan(sp[4]) and np.isnan(sp[5])
+
+
 def test_medium_free_flight_fraction(tmp_path):
     # ConstantMedium.cpp:14-58: a ray crossing a slab of length L inside a medium of density rho
     # scatters with probability 1 - exp(-rho L).
