@@ -33,7 +33,7 @@ class SceneInfo(ctypes.Structure):
                 ("lists", ctypes.c_int), ("xforms", ctypes.c_int), ("media", ctypes.c_int),
                 ("max_stack", ctypes.c_int), ("bvh_depth", ctypes.c_int), ("node_bytes", ctypes.c_uint64),
                 ("acc_lists", ctypes.c_int), ("acc_nodes", ctypes.c_int), ("linear_steps", ctypes.c_int),
-                ("origins_bounded", ctypes.c_int)]
+                ("origins_bounded", ctypes.c_int), ("box_steps", ctypes.c_int)]
 
 
 class CameraDesc(ctypes.Structure):

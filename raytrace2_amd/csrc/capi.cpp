@@ -432,6 +432,7 @@ int rt2_scene_get_info(const rt2_scene* s, rt2_scene_info* o) {
   o->acc_nodes = c.acc_nodes;
   o->linear_steps = (int)(c.lin.size() / 4);
   o->origins_bounded = c.origins_bounded ? 1 : 0;
+  o->box_steps = c.box_steps;
   return RT2_OK;
 }
 

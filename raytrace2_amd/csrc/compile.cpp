@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdint>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
@@ -99,6 +100,56 @@ bool RectAAWords(const float* r, int k, float out[8]) {
   float rec[8] = {r[19], 0, 0, 0, 0, 0, 0, 0};
   if (!CoordRange(r[4 + a], c1, ca, rec[1], rec[2]) || !CoordRange(r[4 + b], c1, cb, rec[3], rec[4])) return false;
   std::copy(rec, rec + 8, out);
+  return true;
+}
+
+// The box step's record (boxaa.h) of a MakeBox run: six QUAD records (node layout, 20 floats each) in the
+// order z+ x+ z- x- y+ y- (Quad.hpp:43-48), each a unit-normal rectangle with QUADAA test words. Words:
+// the six planes per axis (lo, hi: the faces' sD), then on each coordinate the intersection of the four
+// faces' interior ranges on it; mB = 2^-21 B + s (B = max |plane|, s = the largest distance of a face's
+// interior bound from the plane of the box it approximates, rounded up). False unless the faces are a
+// box (lo < hi per axis, the lo faces at the face map's indices, a nonempty inner box) with s <= 2^-20 B,
+// the bound the kernel's margin assumes (DESIGN.md §4 "Box-level test").
+bool BoxAAWordsOf(const float* const face[6], float out[12], float& mB) {
+  static const int kAxis[6] = {2, 0, 2, 0, 1, 1};
+  float tw[6][8];
+  for (int j = 0; j < 6; j++) {
+    uint32_t code;
+    memcpy(&code, &face[j][11], 4);
+    if (code != 4u + (uint32_t)kAxis[j] || !RectAAWords(face[j], kAxis[j], tw[j])) return false;
+  }
+  // planes: lo / hi face index per axis (boxaa.h kBoxAAFaceMap: x- 3, x+ 1, y- 5, y+ 4, z- 2, z+ 0)
+  const int lo_face[3] = {3, 5, 2}, hi_face[3] = {1, 4, 0};
+  float plane[6];
+  double B = 0;
+  for (int k = 0; k < 3; k++) {
+    plane[2 * k] = tw[lo_face[k]][0];
+    plane[2 * k + 1] = tw[hi_face[k]][0];
+    if (!(plane[2 * k] < plane[2 * k + 1])) return false;
+    B = std::max(B, std::max(std::fabs((double)plane[2 * k]), std::fabs((double)plane[2 * k + 1])));
+  }
+  float inner[6];
+  double slack = 0;
+  for (int j = 0; j < 3; j++) {
+    float ilo = -INFINITY, ihi = INFINITY;
+    for (int f = 0; f < 6; f++) {
+      const int k = kAxis[f];
+      if (k == j) continue;
+      const int slot = (j == (k + 1) % 3) ? 1 : 3;  // test words: sD, lo[A], hi[A], lo[B], hi[B]
+      const float lo = tw[f][slot], hi = tw[f][slot + 1];
+      ilo = std::max(ilo, lo);
+      ihi = std::min(ihi, hi);
+      slack = std::max(slack, std::fabs((double)lo - (double)plane[2 * j]));
+      slack = std::max(slack, std::fabs((double)hi - (double)plane[2 * j + 1]));
+    }
+    if (!(ilo <= ihi)) return false;
+    inner[2 * j] = ilo;
+    inner[2 * j + 1] = ihi;
+  }
+  if (!(B > 0) || !(B <= 0x1p100) || !(slack <= 0x1p-20 * B)) return false;
+  std::copy(plane, plane + 6, out);
+  std::copy(inner, inner + 6, out + 6);
+  mB = std::nextafter((float)(0x1p-21 * B + slack), INFINITY);
   return true;
 }
 
@@ -586,6 +637,27 @@ struct Flattener {
     const Obj& o = s.objs[(size_t)i];
     return inside(o.aabb) && inside(s.objs[(size_t)o.child].aabb) && inside(s.objs[(size_t)s.root].aabb);
   }
+  // Box-level steps (boxaa.h) for scenes with spheres: their kernels (render.hip BoxOn) take them; the
+  // sphere-free kernels (the Cornell boxes) run the six-face runs, which measured cheaper there (DESIGN.md
+  // §4 "Box-level test"). RT2_BOX_AA=0 keeps every MakeBox a plain run, 1 forces the steps (tests).
+  bool box_aa = false;
+  void SetBoxAA() {
+    bool spheres = false;
+    for (const Obj& o : s.objs) spheres = spheres || o.kind == kSphere;
+    box_aa = spheres;
+    if (const char* e = getenv("RT2_BOX_AA")) box_aa = atoi(e) != 0 && (spheres || atoi(e) == 2);
+  }
+  // A list that is a MakeBox whose faces all take the QUADAA rectangle test in this space: its box words
+  bool BoxList(const Obj& o, uint32_t parent_xf, const std::vector<float>& lind, float bw[12], float& mB) const {
+    if (o.kind != kList || o.children.size() != 6 || !QuadAASpace(parent_xf, lind)) return false;
+    const float* faces[6];
+    for (int j = 0; j < 6; j++) {
+      const int c = o.children[(size_t)j];
+      if (s.objs[(size_t)c].kind != kQuad) return false;
+      faces[j] = out.nodes.data() + 4 * (size_t)(ref_of.at(c) & kOffsetMask);
+    }
+    return BoxAAWordsOf(faces, bw, mB);
+  }
   bool ContainsAccList(int i) const {
     const Obj& o = s.objs[(size_t)i];
     if (o.kind == kList && acc_depth.count(i)) return true;
@@ -632,9 +704,28 @@ struct Flattener {
           lin[4 * me + 1] = (uint32_t)(lin.size() / 4);
           return true;
         }
-        for (int c : o.children)
-          if (!Linearize(c, parent_xf, lin, lind, xf_depth)) return false;
-        return true;
+        {
+          // a MakeBox list (Quad.hpp:34-50) whose six faces take the QUADAA test: a kBoxAA step before
+          // its run (boxaa.h: the box-level test; skip = past the run, which certified lanes skip and the
+          // others run), its 12 record words right before the faces' records (the run's first face record
+          // is the step's record + 3), aux = the margin constant mB
+          size_t box = SIZE_MAX;
+          float bw[12], mB;
+          if (box_aa && BoxList(o, parent_xf, lind, bw, mB)) {
+            const uint32_t rec = (uint32_t)(lind.size() / 4);
+            lind.insert(lind.end(), bw, bw + 12);
+            uint32_t mbits;
+            memcpy(&mbits, &mB, 4);
+            box = emit(kBoxAA, rec, mbits);
+          }
+          for (int c : o.children)
+            if (!Linearize(c, parent_xf, lin, lind, xf_depth)) return false;
+          if (box != SIZE_MAX) {
+            lin[4 * box + 1] = (uint32_t)(lin.size() / 4);
+            out.box_steps++;
+          }
+          return true;
+        }
       case kXform: {
         uint32_t off = CopyRecords(src, kXformRecords, lind);
         lind[4 * (off + 1) + 3] = Bits(parent_xf);
@@ -777,6 +868,7 @@ void PackTextures(const Scene& s, CompiledScene& out) {
 }  // namespace
 
 bool QuadAATestWords(const float* r, int k, float out[8]) { return RectAAWords(r, k, out); }
+bool BoxAAWords(const float* const faces[6], float out[12], float& mB) { return BoxAAWordsOf(faces, out, mB); }
 
 bool CompileScene(const Scene& s, CompiledScene& out, std::string& err, bool accelerate_lists) {
   return CompileSceneWith(s, out, err, accelerate_lists, kAccDepthSlack);
@@ -838,6 +930,7 @@ bool CompileSceneWith(const Scene& s, CompiledScene& out, std::string& err, bool
     err = "scene too large for 28-bit node offsets";
     return false;
   }
+  fl.SetBoxAA();
   if (!fl.Linearize(s.root, kRefNone, out.lin, out.lind)) {
     out.lin.clear();
     out.lind.clear();
@@ -857,7 +950,7 @@ bool CompileSceneWith(const Scene& s, CompiledScene& out, std::string& err, bool
     size_t n = out.lin.size() / 4;
     std::vector<char> entry(n + 1, 0);
     for (size_t i = 0; i < n; i++)
-      if (out.lin[4 * i] == kBvh || out.lin[4 * i] == kAccBvh) entry[out.lin[4 * i + 1]] = 1;
+      if (out.lin[4 * i] == kBvh || out.lin[4 * i] == kAccBvh || out.lin[4 * i] == kBoxAA) entry[out.lin[4 * i + 1]] = 1;
     for (size_t i = n; i-- > 0;) {
       if (out.lin[4 * i] != kQuad) continue;
       uint32_t run = 1;

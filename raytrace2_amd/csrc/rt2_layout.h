@@ -29,6 +29,7 @@ enum NodeKind : uint32_t {
   kAccSphere = 11, // a sphere reached through a list's acceleration tree
   kQuadAA = 12,    // threaded program only: a unit-normal axis-aligned quad in the QUADAA layout
   kProgramEnd = 13,  // threaded program only: the wide program's entry at index lin_len (no step)
+  kBoxAA = 14,     // threaded program only: the box-level test of the MakeBox run that follows (boxaa.h)
 };
 inline constexpr bool is_acc_bvh(uint32_t kind) { return kind - kAccBvh < 3u; }
 constexpr int kListAccelMin = 32;  // leaf-only sphere lists at least this long get a tree

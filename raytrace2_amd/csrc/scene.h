@@ -145,6 +145,7 @@ struct CompiledScene {
   int lin_xform_depth = 0;        // deepest transform nesting in the threaded program (0: none)
   int bvh_nodes = 0, quads = 0, spheres = 0, lists = 0, xforms = 0, media = 0;
   int acc_lists = 0, acc_nodes = 0;  // exact list acceleration trees (rt2_layout.h LISTACC)
+  int box_steps = 0;                 // MakeBox runs given a box-level test step (boxaa.h, kBoxAA)
   int bvh_depth = 0;
   uint32_t features = 0;          // rt2_layout.h Feature bits (defocus is added per render)
   // The threaded program uses a test that is exact only for ray origins within +-2^64 in world space
@@ -167,6 +168,10 @@ bool CompileSceneWith(const Scene& s, CompiledScene& out, std::string& err, bool
 // The 8 QUADAA test words of QUAD record r (20 floats, rt2_layout.h) with axis code k + 4, or false when
 // the quad takes the general path (compile.cpp RectAAWords; for tests/cpp/quadaa_bounds.cpp).
 bool QuadAATestWords(const float* r, int k, float out[8]);
+// The box step's 12 record words and margin constant (boxaa.h) of six QUAD records in MakeBox order, or
+// false when they are not a box the box-level test can take (compile.cpp BoxAAWordsOf; for
+// tests/cpp/box_cert.cpp).
+bool BoxAAWords(const float* const faces[6], float out[12], float& mB);
 
 // Philox4x32-10 (shared constants with the kernel; see render.hip)
 void Philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1);

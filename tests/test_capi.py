@@ -81,6 +81,28 @@ def test_paired_program_steps_are_well_formed(tmp_path, scene, expect):
     assert r.stdout.startswith("pairs=")
 
 
+def test_box_level_test_decides_as_the_six_face_run(tmp_path):
+    """boxaa.h BoxAATest (the kernel's kBoxAA step, host only): on random MakeBox boxes compiled by the
+    product, for rays entering through faces, edges and corners, grazing, leaving a face from a rounded
+    hit point, starting inside, passing near and with zero direction components, every lane the box test
+    certifies gets exactly the six-face run's answer (face and final interval key); the certified
+    fractions are printed (tests/cpp/box_cert.cpp)."""
+    csrc = os.path.join(ROOT, "raytrace2_amd", "csrc")
+    exe = str(tmp_path / "box_cert")
+    r = subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
+                        "-I", csrc, "-o", exe, os.path.join(ROOT, "tests", "cpp", "box_cert.cpp")]
+                       + [os.path.join(csrc, f) for f in ("json.cpp", "scene.cpp", "compile.cpp")],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
+    for seed in (1, 2):
+        r = subprocess.run([exe, "300", "12000", str(seed), str(tmp_path)], capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr + r.stdout
+        assert "boxes=" in r.stdout
+        cert = {l.split(" rays")[0].strip(): float(l.split()[-1]) for l in r.stdout.splitlines()
+                if "certified" in l and not l.startswith("boxes")}
+        assert cert["enter face"] > 0.9 and cert["inside"] > 0.99, cert
+
+
 def test_quadaa_bounds_decide_as_quad_hit(tmp_path):
     """compile.cpp CoordRange (host only): the kernel's QUADAA interior test, lo <= p <= hi on the hit
     point's two in-plane coordinates, decides as Quad::Hit's alpha/beta test (Quad.cpp:27-36) for
