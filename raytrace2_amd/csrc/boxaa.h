@@ -1,6 +1,6 @@
 // boxaa.h — the box-level test of a MakeBox run (Quad.hpp:34-50: a HittableList of six quads, the faces
-// z+ x+ z- x- y+ y- of an axis-aligned box in its own space), shared by the kernel (render.hip, kBoxAA
-// steps) and its host proof harness (tests/cpp/box_cert.cpp). The includer defines RT2_BOXAA_FN (the
+// z+ x+ z- x- y+ y- of an axis-aligned box in its own space), shared by the kernel (render.hip: the quad-run
+// step of a box-flagged run) and its host proof harness (tests/cpp/box_cert.cpp). The includer defines RT2_BOXAA_FN (the
 // function qualifiers) and passes a math policy M: min / max / min3 / max3 / med3 of non-NaN floats, fma,
 // and the division by a correctly rounded reciprocal (render.hip div_by_inv). Every operation is
 // correctly rounded IEEE single precision on both sides, so both compute the same bits.
@@ -18,11 +18,11 @@
 
 namespace rt2 {
 
-// The box step's 12 record words (the 48 bytes the wide program carries inline):
+// The box record (16 words right before the run's first face record; compile.cpp BoxAAWordsOf):
 //   [0..5]  face planes lo_x, hi_x, lo_y, hi_y, lo_z, hi_z (the faces' sD words: x- x+ y- y+ z- z+)
 //   [6..11] inner bounds in_lo_x, in_hi_x, in_lo_y, in_hi_y, in_lo_z, in_hi_z: on each coordinate the
 //           intersection of the four faces' QUADAA interior ranges on it (compile.cpp BoxAAWords)
-// and its aux word: mB = 2^-21 max|plane| + s, s the largest distance of a face's interior bound from the
+//   [12]    mB = 2^-21 max|plane| + s, s the largest distance of a face's interior bound from the
 // box plane it approximates (the compiler requires s <= 2^-20 max|plane|).
 constexpr int kBoxAAWords = 12;
 // Face indices within the MakeBox run (z+ x+ z- x- y+ y-) of face (axis K, hi side): 3 bits each,

@@ -11,6 +11,10 @@
 #include <unordered_set>
 
 #include "scene.h"
+#ifndef RT2_BOXAA_FN
+#define RT2_BOXAA_FN inline
+#endif
+#include "boxaa.h"
 
 namespace rt2 {
 
@@ -641,6 +645,7 @@ struct Flattener {
   // sphere-free kernels (the Cornell boxes) run the six-face runs, which measured cheaper there (DESIGN.md
   // §4 "Box-level test"). RT2_BOX_AA=0 keeps every MakeBox a plain run, 1 forces the steps (tests).
   bool box_aa = false;
+  std::vector<uint32_t> box_runs;  // first quad step of each MakeBox run with a box record
   void SetBoxAA() {
     bool spheres = false;
     for (const Obj& o : s.objs) spheres = spheres || o.kind == kSphere;
@@ -705,25 +710,22 @@ struct Flattener {
           return true;
         }
         {
-          // a MakeBox list (Quad.hpp:34-50) whose six faces take the QUADAA test: a kBoxAA step before
-          // its run (boxaa.h: the box-level test; skip = past the run, which certified lanes skip and the
-          // others run), its 12 record words right before the faces' records (the run's first face record
-          // is the step's record + 3), aux = the margin constant mB
-          size_t box = SIZE_MAX;
-          float bw[12], mB;
-          if (box_aa && BoxList(o, parent_xf, lind, bw, mB)) {
-            const uint32_t rec = (uint32_t)(lind.size() / 4);
-            lind.insert(lind.end(), bw, bw + 12);
-            uint32_t mbits;
-            memcpy(&mbits, &mB, 4);
-            box = emit(kBoxAA, rec, mbits);
+          // a MakeBox list (Quad.hpp:34-50) whose six faces take the QUADAA test: its box record (boxaa.h:
+          // 12 words, then mB, padded to 4 records) right before the faces' records, and its first quad
+          // step noted; after the run pass its run (exactly these six quads) gets the box flag (aux bit
+          // 31), and the kernel runs the box-level test before the six-face run
+          if (box_aa) {
+            float bw[12], mB;
+            if (BoxList(o, parent_xf, lind, bw, mB)) {
+              float rec[16] = {};
+              std::copy(bw, bw + 12, rec);
+              rec[12] = mB;
+              lind.insert(lind.end(), rec, rec + 16);
+              box_runs.push_back((uint32_t)(lin.size() / 4));
+            }
           }
           for (int c : o.children)
             if (!Linearize(c, parent_xf, lin, lind, xf_depth)) return false;
-          if (box != SIZE_MAX) {
-            lin[4 * box + 1] = (uint32_t)(lin.size() / 4);
-            out.box_steps++;
-          }
           return true;
         }
       case kXform: {
@@ -950,7 +952,8 @@ bool CompileSceneWith(const Scene& s, CompiledScene& out, std::string& err, bool
     size_t n = out.lin.size() / 4;
     std::vector<char> entry(n + 1, 0);
     for (size_t i = 0; i < n; i++)
-      if (out.lin[4 * i] == kBvh || out.lin[4 * i] == kAccBvh || out.lin[4 * i] == kBoxAA) entry[out.lin[4 * i + 1]] = 1;
+      if (out.lin[4 * i] == kBvh || out.lin[4 * i] == kAccBvh) entry[out.lin[4 * i + 1]] = 1;
+    for (uint32_t b : fl.box_runs) entry[b] = entry[b + 6] = 1;  // a box's run is its six quads exactly
     for (size_t i = n; i-- > 0;) {
       if (out.lin[4 * i] != kQuad) continue;
       uint32_t run = 1;
@@ -966,6 +969,14 @@ bool CompileSceneWith(const Scene& s, CompiledScene& out, std::string& err, bool
       const uint32_t run = out.lin[4 * i + 3];
       for (uint32_t k = 0; k < run; k++) codes |= fl.lind_axis.at(out.lin[4 * (i + k) + 2]) << (3 * k);
       out.lin[4 * i + 1] = codes | (1u << (3 * run));
+    }
+    for (uint32_t b : fl.box_runs) {
+      if (out.lin[4 * b] != kQuad || out.lin[4 * b + 3] != 6u || out.lin[4 * b + 1] != kBoxAARunCodes) {
+        err = "internal: a box's quads did not form its run";
+        return false;
+      }
+      out.lin[4 * b + 3] |= kRunBoxFlag;
+      out.box_steps++;
     }
   }
   // Wide program: each 16-byte step entry followed by the first 48 bytes of its record (a whole BVH

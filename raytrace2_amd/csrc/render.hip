@@ -1509,9 +1509,9 @@ __device__ __forceinline__ uint32_t wave_min_next(uint32_t next) {
   return i;
 }
 
-// kBoxAA steps run in the sphere kernels (the compiler emits them only for scenes with spheres: book 2's
-// ground boxes, DESIGN.md §4 "Box-level test"); early in the step dispatch where lists of boxes are common
-// (book 2: accelerated lists), last otherwise.
+// The box-level test of box-flagged MakeBox runs runs in the sphere kernels (the compiler flags runs only
+// in scenes with spheres: book 2's ground boxes; the Cornell box kernel measured its two boxes' runs cheaper
+// than the test, DESIGN.md §4 "Box-level test").
 template <uint32_t F>
 constexpr bool BoxOn() {
   return Has<F, kFeatSphere>();
@@ -1536,7 +1536,6 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
   f3 acc_pinv = mk(0.0f, 0.0f, 0.0f);  // accelerated list: this ray's box padding x inv
   uint32_t acc_best = kRefNone;  // accelerated list: child index of its current closest sphere
   uint32_t next = 0;  // this lane's next step
-  constexpr bool kBoxEarly = BoxOn<F>() && Has<F, kFeatAccList>(), kBoxLate = BoxOn<F>() && !kBoxEarly;
   RT2_WAVE(0);
 #if RT2_EXP_WAVESTEPS
   cnt.wd[7]++;
@@ -1599,31 +1598,38 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
     if (kind == kMedium) RT2_WAVE(5);
     const uint32_t at = i;
     i = kRefNone;  // computed after the step
-    // A MakeBox run's box-level test (boxaa.h; compile.cpp emits kBoxAA steps only for scenes with
-    // spheres, whose kernels all take them): a certified lane takes the candidate face's answer and
-    // skips the six-face run that follows; the others run it (next = at + 1). The step's inline words are
-    // the box record, aux = the margin constant, and the run's first face record is the step's record + 3.
-    auto box_step = [&]() {
-      float bw[kBoxAAWords];
-#pragma unroll
-      for (int j = 0; j < kBoxAAWords; j++) bw[j] = uf(sw[4 + j]);
-      const uint32_t kmax0 = bits(tmax) - bits(tmin);
-      const BoxAAResult r = BoxAATest<BoxMath>(bw, uf(st.w), o.x, o.y, o.z, d.x, d.y, d.z, inv.x, inv.y, inv.z, tmin, kmax0);
-      if (r.cert) {
-        if (kStats) cnt.quad += 6;  // the run's six Quad::Hit tests (the reference's count)
-        if (r.x <= kmax0) {
-          tmax = r.t;
-          prim = make_ref(kQuadAA, off + 3u + r.face * (uint32_t)kQuadRecords);
-        }
-        next = st.y;
-      }
-    };
     if (next == at) {
     next = at + 1u;
     if (kind == kQuad) {
       // a run of st.w quads with contiguous records, axis codes in st.y (3 bits each), tested in
       // order (issue-bound: one candidate at a time beats two interleaved, measured)
-      const uint32_t run = st.w;
+      const uint32_t run = st.w & kRunLenMask;
+      // A MakeBox run with a box record (aux bit 31; compile.cpp, for scenes with spheres): the box-level
+      // test (boxaa.h) first. A certified lane takes the candidate face's answer and skips the run; the
+      // wave runs the six faces only for the lanes it could not certify. The box record (12 words) lies
+      // right before the run's first face record; aux = run | flag, the margin constant in the record's
+      // trailing word (compile.cpp BoxAAWordsOf).
+      bool boxed = false;
+      if constexpr (BoxOn<F>()) {
+        if ((int)st.w < 0) {
+          const u32x16 bwr = sld16(recs, (off - 4u) * 16u);
+          float bw[kBoxAAWords];
+#pragma unroll
+          for (int j = 0; j < kBoxAAWords; j++) bw[j] = uf(bwr[j]);
+          const uint32_t kmax0 = bits(tmax) - bits(tmin);
+          const BoxAAResult r =
+              BoxAATest<BoxMath>(bw, uf(bwr[12]), o.x, o.y, o.z, d.x, d.y, d.z, inv.x, inv.y, inv.z, tmin, kmax0);
+          if (r.cert) {
+            if (kStats) cnt.quad += 6;  // the run's six Quad::Hit tests (the reference's count)
+            if (r.x <= kmax0) {
+              tmax = r.t;
+              prim = make_ref(kQuadAA, off + r.face * (uint32_t)kQuadRecords);
+            }
+            boxed = true;
+          }
+        }
+      }
+      if (!boxed) {
       uint32_t codes = st.y;  // 3 bits per quad, then a 1 bit (compile.cpp)
       // the run's interval test in_interval(t, tmin, tmax) as key(t) <= kmax with key(x) = bits(x) -
       // bits(tmin) (kmax = key(tmax), updated with the accepted t's key; tmax = its float after the run)
@@ -1734,9 +1740,8 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
         vref += (uint32_t)kQuadRecords;
       }
       tmax = uf(kmax + bits(tmin));
+      }  // !boxed
       next = at + run;
-    } else if (kBoxEarly && kind == kBoxAA) {
-      box_step();
     } else if (Has<F, kFeatSphere>() && kind == kSphere) {
       float t;
       uint32_t ref = make_ref(kind, off);
@@ -1929,8 +1934,6 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
         prim = make_ref(kMedium, off);
         h.xf = cur_xf;
       }
-    } else if (kBoxLate && kind == kBoxAA) {
-      box_step();
     }
     }  // next == at
     i = wave_min_next(next);

@@ -29,7 +29,6 @@ enum NodeKind : uint32_t {
   kAccSphere = 11, // a sphere reached through a list's acceleration tree
   kQuadAA = 12,    // threaded program only: a unit-normal axis-aligned quad in the QUADAA layout
   kProgramEnd = 13,  // threaded program only: the wide program's entry at index lin_len (no step)
-  kBoxAA = 14,     // threaded program only: the box-level test of the MakeBox run that follows (boxaa.h)
 };
 inline constexpr bool is_acc_bvh(uint32_t kind) { return kind - kAccBvh < 3u; }
 constexpr int kListAccelMin = 32;  // leaf-only sphere lists at least this long get a tree
@@ -186,6 +185,9 @@ constexpr int kLinearMaxSteps = 1 << 16;
 #define RT2_LINEAR_MAX_RUN 10
 #endif
 constexpr uint32_t kLinearMaxRun = RT2_LINEAR_MAX_RUN;  // quads per run (3-bit axis codes + 1 bit in one word)
+// A quad step's aux word: the run length, and bit 31 for a MakeBox run whose box record (boxaa.h, 16 words:
+// the 12 box words, the margin constant, padding) lies right before the run's first face record
+constexpr uint32_t kRunLenMask = 0xFFu, kRunBoxFlag = 0x80000000u;
 static_assert(3 * kLinearMaxRun < 32, "a run's codes and their end bit fit one word");
 constexpr int kLinearMaxXformDepth = 8;  // deeper transform nesting uses the stack traversal
 

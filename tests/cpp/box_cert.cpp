@@ -1,8 +1,9 @@
-// Host proof check of the box-level MakeBox test (boxaa.h BoxAATest, the kernel's kBoxAA step):
+// Host proof check of the box-level MakeBox test (boxaa.h BoxAATest, run by the kernel before a flagged
+// MakeBox quad run, render.hip):
 //   box_cert <n_boxes> <rays_per_box> <seed> <scratch_dir>
 // Random boxes (MakeBox, Quad.hpp:34-50: corners from 2^-6 to 2^12, thin and flat boxes, boxes far from
 // the origin) are written as a scene, loaded and compiled by the product (scene.cpp, compile.cpp), and
-// for every kBoxAA step of the compiled program the box test is compared with the six-face run it
+// for every box-flagged run of the compiled program the box test is compared with the six-face run it
 // stands for, executed as the kernel executes it (render.hip quad_aa: each face's t, hit point and
 // QUADAA rejection word; accepted iff key | rejection <= kmax, later faces winning ties), on rays that
 // stress the certificate: entering through face interiors, edges and corners (on them and a few ulps
@@ -135,22 +136,22 @@ int main(int argc, char** argv) {
   }
   std::vector<Box> boxes;
   const size_t n = c.lin.size() / 4;
-  for (size_t i = 0; i + 1 < n; i++) {
-    if (c.lin[4 * i] != kBoxAA) continue;
+  for (size_t i = 0; i < n; i++) {
+    if (c.lin[4 * i] != kQuad || !(c.lin[4 * i + 3] & kRunBoxFlag)) continue;
     Box bx;
-    memcpy(bx.w, &c.lin_wide[16 * i + 4], 48);
-    bx.mB = F(c.lin[4 * i + 3]);
-    const size_t q0 = i + 1;
-    if (c.lin[4 * q0] != kQuad || c.lin[4 * q0 + 3] != 6 || c.lin[4 * q0 + 1] != kBoxAARunCodes) {
-      fprintf(stderr, "box step %zu is not followed by its MakeBox run\n", i);
+    if ((c.lin[4 * i + 3] & kRunLenMask) != 6 || c.lin[4 * i + 1] != kBoxAARunCodes) {
+      fprintf(stderr, "box run at step %zu is not a MakeBox run\n", i);
       return 1;
     }
-    if (c.lin[4 * i + 1] != q0 + 6) {
-      fprintf(stderr, "box step %zu: skip %u is not past its run\n", i, c.lin[4 * i + 1]);
-      return 1;
-    }
+    const size_t rec = c.lin[4 * i + 2];  // the run's first face record; the box record is the 4 before it
+    memcpy(bx.w, &c.lind[4 * (rec - 4)], 48);
+    bx.mB = c.lind[4 * (rec - 4) + 12];
     for (int j = 0; j < 6; j++) {
-      memcpy(bx.tw[j], &c.lind[4 * (size_t)c.lin[4 * (q0 + j) + 2]], 32);
+      if (c.lin[4 * (i + j) + 2] != rec + 5u * (uint32_t)j) {
+        fprintf(stderr, "box run at step %zu: face records are not contiguous\n", i);
+        return 1;
+      }
+      memcpy(bx.tw[j], &c.lind[4 * (size_t)c.lin[4 * (i + j) + 2]], 32);
       bx.axis[j] = (int)((kBoxAARunCodes >> (3 * j)) & 7u) - 4;
     }
     boxes.push_back(bx);

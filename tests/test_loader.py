@@ -52,11 +52,12 @@ def test_scene_compile_facts():
     assert b2.spheres == 1007 and b2.xforms == 1 and b2.media == 2 and b2.quads == 400 * 6 + 1
     # the 1000-sphere list under the transform gets an exact acceleration tree (n - 1 nodes), threaded
     # into the program after its LISTACC step: 1 + 999 + 1000 of the program's 4922 steps
-    # the list's tree (999 nodes + 1000 spheres = 1999 steps) in eight octant-ordered copies, and a
-    # box-level step before each of the 341 ground boxes (of 400) whose six faces take the QUADAA test (the 59
-    # others have x / z faces whose normalized normal is not exactly +-1: compile.cpp BoxAAWordsOf)
+    # the list's tree (999 nodes + 1000 spheres = 1999 steps) in eight octant-ordered copies; a box record
+    # (the box-level test, boxaa.h) for each of the 341 ground boxes (of 400) whose six faces take the QUADAA
+    # test (the 59 others have x / z faces whose normalized normal is not exactly +-1: compile.cpp
+    # BoxAAWordsOf)
     assert (b2.acc_lists, b2.acc_nodes, b2.box_steps) == (1, 999, 341)
-    assert b2.linear_steps == 4922 + 7 * 1999 + 341
+    assert b2.linear_steps == 4922 + 7 * 1999
     assert b2.max_stack <= 24
     assert info.acc_lists == 0 and info.linear_steps > 0
     assert info.box_steps == 0  # sphere-free scenes keep the six-face runs (render.hip BoxOn)
