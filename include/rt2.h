@@ -265,6 +265,10 @@ typedef struct {
    * buffers, chunk tables, a root's gathered image). A multi-GPU tracer: the largest GPU's. */
   uint64_t sample_buffer_bytes;
   uint64_t device_bytes_peak;
+  /* stats mode, the box-level test of MakeBox runs (sphere scenes): lanes tested and certified (the others
+   * fall back to the six-face run), wave visits of a flagged run and those in which the wave ran the six
+   * faces for its uncertified lanes */
+  uint64_t box_tests, box_certified, box_wave_visits, box_wave_runs;
 } rt2_stats;
 RT2_API int rt2_tracer_get_stats(rt2_tracer* tr, rt2_stats* out);
 /* The stats of GPU `part` of a multi-GPU tracer (part 0 of a one-GPU tracer is itself). */

@@ -66,7 +66,11 @@ class Stats(ctypes.Structure):
                                                                            ("host_waits", ctypes.c_uint64),
                                                                            ("launch_ms_sum", ctypes.c_double),
                                                                            ("sample_buffer_bytes", ctypes.c_uint64),
-                                                                           ("device_bytes_peak", ctypes.c_uint64)]
+                                                                           ("device_bytes_peak", ctypes.c_uint64),
+                                                                           ("box_tests", ctypes.c_uint64),
+                                                                           ("box_certified", ctypes.c_uint64),
+                                                                           ("box_wave_visits", ctypes.c_uint64),
+                                                                           ("box_wave_runs", ctypes.c_uint64)]
 
     def as_dict(self):
         d = {n: (getattr(self, n) if n.endswith("_ms") else int(getattr(self, n))) for n, _ in self._fields_

@@ -1600,6 +1600,10 @@ int rt2_tracer_get_stats(rt2_tracer* t, rt2_stats* o) {
       sum.medium_tests += s.medium_tests;
       sum.list_visits += s.list_visits;
       sum.overflow += s.overflow;
+      sum.box_tests += s.box_tests;
+      sum.box_certified += s.box_certified;
+      sum.box_wave_visits += s.box_wave_visits;
+      sum.box_wave_runs += s.box_wave_runs;
       sum.launches = std::max(sum.launches, s.launches);
       sum.kernel_ms = std::max(sum.kernel_ms, s.kernel_ms);
       sum.launch_ms_sum = std::max(sum.launch_ms_sum, s.launch_ms_sum);
@@ -1633,6 +1637,10 @@ int rt2_tracer_get_stats(rt2_tracer* t, rt2_stats* o) {
   o->medium_tests = s[StatsCounters::kMediumTests];
   o->list_visits = s[StatsCounters::kListVisits];
   o->overflow = s[StatsCounters::kCount];
+  o->box_tests = s[StatsCounters::kBoxTests];
+  o->box_certified = s[StatsCounters::kBoxCertified];
+  o->box_wave_visits = s[StatsCounters::kBoxWaveVisits];
+  o->box_wave_runs = s[StatsCounters::kBoxWaveRuns];
   for (int k = 0; k < 4; k++) o->stamps[k] = s[StatsCounters::kStamps + k];
   for (int k = 0; k < 8; k++) o->diag[k] = s[StatsCounters::kDiag + k];
   o->launches = t->launches;

@@ -740,6 +740,7 @@ __device__ __forceinline__ f3 refract(f3 uv, f3 n, float etai_over_etat) {
 
 struct Counters {
   uint32_t bvh, quad, sphere, xform, medium, list;
+  uint32_t box, box_cert, box_wave, box_wave_run;  // box-level test (counting kernels)
 #if RT2_EXP_WAVESTEPS
   // wave-level (counted by the first active lane): trace calls, steps, bvh + acc-bvh steps, quad
   // runs, sphere + acc-sphere steps, media, extra trips of the min-index search, active lanes at
@@ -1619,8 +1620,17 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
           const uint32_t kmax0 = bits(tmax) - bits(tmin);
           const BoxAAResult r =
               BoxAATest<BoxMath>(bw, uf(bwr[12]), o.x, o.y, o.z, d.x, d.y, d.z, inv.x, inv.y, inv.z, tmin, kmax0);
+          if (kStats) {
+            cnt.box++;
+            const bool lead = (int)__lane_id() == __builtin_amdgcn_readfirstlane((int)__lane_id());
+            cnt.box_wave += lead ? 1u : 0u;
+            cnt.box_wave_run += (lead && !__all(r.cert)) ? 1u : 0u;
+          }
           if (r.cert) {
-            if (kStats) cnt.quad += 6;  // the run's six Quad::Hit tests (the reference's count)
+            if (kStats) {
+              cnt.quad += 6;  // the run's six Quad::Hit tests (the reference's count)
+              cnt.box_cert++;
+            }
             if (r.x <= kmax0) {
               tmax = r.t;
               prim = make_ref(kQuadAA, off + r.face * (uint32_t)kQuadRecords);
@@ -2649,6 +2659,12 @@ __global__ __launch_bounds__(kBlock, (MinWaves<F, kMode, kStats>())) void render
     atomicAdd(P.stats + StatsCounters::kXformVisits, (unsigned long long)cnt.xform);
     atomicAdd(P.stats + StatsCounters::kMediumTests, (unsigned long long)cnt.medium);
     atomicAdd(P.stats + StatsCounters::kListVisits, (unsigned long long)cnt.list);
+    if (BoxOn<F>()) {
+      atomicAdd(P.stats + StatsCounters::kBoxTests, (unsigned long long)cnt.box);
+      atomicAdd(P.stats + StatsCounters::kBoxCertified, (unsigned long long)cnt.box_cert);
+      atomicAdd(P.stats + StatsCounters::kBoxWaveVisits, (unsigned long long)cnt.box_wave);
+      atomicAdd(P.stats + StatsCounters::kBoxWaveRuns, (unsigned long long)cnt.box_wave_run);
+    }
   }
   if (overflow) atomicAdd(P.stats + StatsCounters::kCount, 1ull);  // overflow flag slot
   // the launch's last-wave end

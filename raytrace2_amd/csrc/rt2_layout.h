@@ -206,6 +206,9 @@ struct CameraParams {
 struct StatsCounters {  // u64 slots written by the kernel
   enum { kRays = 0, kBvhTests, kQuadTests, kSphereTests, kXformVisits, kMediumTests, kListVisits, kPaths, kCount };
   enum { kOverflow = kCount, kStamps = 9, kDiag = 16, kSlots = 32 };  // stamps / diag: diagnostic builds
+  // the box-level test of flagged MakeBox runs (boxaa.h): lanes tested, lanes certified; wave visits of
+  // a flagged run, and those in which some lane fell back so the wave ran the six faces
+  enum { kBoxTests = 24, kBoxCertified, kBoxWaveVisits, kBoxWaveRuns };
 };
 constexpr int kStatsSlots = StatsCounters::kSlots;
 

@@ -118,9 +118,10 @@ def test_book2_trace_loops_keep_the_scalar_issue_code_generation(isa):
     """the book 2 kernel's loop shapes under the two LLVM options of the Makefile, as
     for the Cornell kernel below. Its quad-run loop (the ground's MakeBox runs, a third of C5's time:
     the depth-3 loop with a scalar record load and v_or3 rejection words) holds three separate QUADAA
-    interior tests (6 v_or3), no exec-mask save per quad and at most 28 SALU (22); its BVH-step loop at
-    most 32 SALU (27); its trace loop at most 400 SALU (361; 586 without -structurizecfg-skip-uniform-regions,
-    and without -simplifycfg-sink-common=false the quad bodies merge into one: 2 v_or3)."""
+    interior tests (6 v_or3), no exec-mask save per quad and at most 28 SALU (23); its BVH-step loop at
+    most 32 SALU (27); its trace loop, which holds the box-level test of flagged MakeBox runs (boxaa.h), at
+    most 440 SALU (409; 361 before the box test; 586 without -structurizecfg-skip-uniform-regions, and
+    without -simplifycfg-sink-common=false the quad bodies merge into one: 2 v_or3)."""
     _, body = _kernel(isa, "ILj815ELi2ELb0E")
     loops = _loops(body)
     quad = [(h, c) for h, d, c in loops if d == 3 and c["v_or3_b32"] > 0 and any(k.startswith("s_load") for k in c)]
@@ -130,7 +131,7 @@ def test_book2_trace_loops_keep_the_scalar_issue_code_generation(isa):
     assert c["s_and_saveexec_b64"] == 0, c["s_and_saveexec_b64"]
     assert _salu(c) <= 28, _salu(c)
     trace = [(h, c) for h, d, c in loops if d == 2 and _salu(c) > 60]
-    assert len(trace) == 1 and _salu(trace[0][1]) <= 400, [_salu(c) for _, c in trace]
+    assert len(trace) == 1 and _salu(trace[0][1]) <= 440, [_salu(c) for _, c in trace]
     # the BVH-step run: the first depth-3 loop nested in the trace loop
     bvh = [c for h, d, c in loops if d == 3 and c["v_or3_b32"] == 0 and _salu(c) > 10]
     assert bvh and _salu(bvh[0]) <= 32, [_salu(c) for c in bvh]
