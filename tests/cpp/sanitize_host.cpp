@@ -114,7 +114,8 @@ int main(int argc, char** argv) {
     const std::string text = ReadAll(p);
     const std::string tmp = out + "/fuzz.json";
     // every byte prefix of the small documents (a stride through the large ones)
-    const size_t stride = text.size() <= 4096 ? 1 : text.size() / 509;
+    const bool small = text.size() <= 4096;
+    const size_t stride = small ? 1 : text.size() / 61;
     for (size_t n = 0; n < text.size(); n += stride) {
       WriteAll(tmp, text.substr(0, n));
       accepted += Exercise(tmp, false);
@@ -123,7 +124,7 @@ int main(int argc, char** argv) {
     // single-byte corruptions: structural characters and digits replaced by JSON-significant bytes
     const char subst[] = {'"', '}', ']', '[', '{', ',', ':', '-', 'e', '0', '\\', '\0'};
     uint64_t x = 0x9E3779B97F4A7C15ull;
-    for (int k = 0; k < 400; k++) {
+    for (int k = 0; k < (small ? 400 : 60); k++) {
       x ^= x << 13;
       x ^= x >> 7;
       x ^= x << 17;

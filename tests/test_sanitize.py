@@ -67,4 +67,4 @@ def test_host_code_is_clean_under_asan_and_ubsan(sanitized, tmp_path):
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-6000:])
     assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr, r.stderr[-6000:]
     assert r.stdout.startswith("documents=")
-    assert int(r.stdout.split()[0].split("=")[1]) > 5000
+    assert int(r.stdout.split()[0].split("=")[1]) > 5000  # (every scene, its prefixes and corruptions)
