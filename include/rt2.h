@@ -117,7 +117,7 @@ RT2_API int rt2_tracer_set_partition(rt2_tracer* tr, int band_h, int rank, int w
 RT2_API int rt2_tracer_set_launch_frames(rt2_tracer* tr, int frames_per_launch); /* 0 = all */
 /* Work split: a launch's frames are cut into chunks and every (pixel, chunk) is one work item. A
  * chunk starting with R frames left holds about R * pixels / (k * resident GPU lanes) frames, k =
- * `items_per_lane` (default 16), at least 1 and at most 64 (RT2_CHUNK_MAX): long items early, short
+ * `items_per_lane` (default 4), at least 1 and at most 64 (RT2_CHUNK_MAX): long items early, short
  * ones at the end of the launch. 0 = one chunk (each pixel's frames in one item). Every frame's
  * sample goes to a per-frame buffer and is summed in frame order after the launch, so results do
  * not depend on the split. `bytes` bounds the device memory the samples take on each GPU in total

@@ -123,7 +123,10 @@ struct rt2_tracer {
   size_t sample_budget = kDefaultSampleBudget;
   size_t scene_bytes = 0;         // scene program, tables and small per-tracer buffers on the device
   size_t device_bytes_peak = 0;   // high-water mark of DeviceBytes()
-  int work_split = 16;                     // chunk schedule: work left split into >= k items per lane (0: one chunk)
+  // chunk schedule: work left split into >= k items per lane (0: one chunk). 4 since round 6: a launch with
+  // few pixels per lane (an 8-way rank) gets 60-frame chunks instead of 12 (emulated 8-way C2 job +4.8 %);
+  // full-size launches are capped at 64-frame chunks either way
+  int work_split = 4;
   int chunk_max = 64;                      // longest chunk (frames)
   int frame_tiles_env = -1;                // RT2_FRAME_TILES: -1 auto, 0 off, 1 on
   bool frame_tiles = false;                // this launch: items = one pixel x 64 short chunks per wave
