@@ -109,12 +109,11 @@ bool RectAAWords(const float* r, int k, float out[8]) {
 
 // The box step's record (boxaa.h) of a MakeBox run: six QUAD records (node layout, 20 floats each) in the
 // order z+ x+ z- x- y+ y- (Quad.hpp:43-48), each a unit-normal rectangle with QUADAA test words. Words:
-// the six planes per axis (lo, hi: the faces' sD), then on each coordinate the intersection of the four
-// faces' interior ranges on it; mB = 2^-21 B + s (B = max |plane|, s = the largest distance of a face's
-// interior bound from the plane of the box it approximates, rounded up). False unless the faces are a
-// box (lo < hi per axis, the lo faces at the face map's indices, a nonempty inner box) with s <= 2^-20 B,
+// the six planes per axis (lo, hi: the faces' sD); mB = 2^-21 B + s (B = max |plane|, s = the largest
+// distance of a face's interior bound from the plane of the box it approximates, rounded up). False
+// unless the faces are a box (lo < hi per axis, the lo faces at the face map's indices) with s <= 2^-20 B,
 // the bound the kernel's margin assumes (DESIGN.md §4 "Box-level test").
-bool BoxAAWordsOf(const float* const face[6], float out[12], float& mB) {
+bool BoxAAWordsOf(const float* const face[6], float out[6], float& mB) {
   static const int kAxis[6] = {2, 0, 2, 0, 1, 1};
   float tw[6][8];
   for (int j = 0; j < 6; j++) {
@@ -132,27 +131,19 @@ bool BoxAAWordsOf(const float* const face[6], float out[12], float& mB) {
     if (!(plane[2 * k] < plane[2 * k + 1])) return false;
     B = std::max(B, std::max(std::fabs((double)plane[2 * k]), std::fabs((double)plane[2 * k + 1])));
   }
-  float inner[6];
   double slack = 0;
   for (int j = 0; j < 3; j++) {
-    float ilo = -INFINITY, ihi = INFINITY;
     for (int f = 0; f < 6; f++) {
       const int k = kAxis[f];
       if (k == j) continue;
       const int slot = (j == (k + 1) % 3) ? 1 : 3;  // test words: sD, lo[A], hi[A], lo[B], hi[B]
       const float lo = tw[f][slot], hi = tw[f][slot + 1];
-      ilo = std::max(ilo, lo);
-      ihi = std::min(ihi, hi);
       slack = std::max(slack, std::fabs((double)lo - (double)plane[2 * j]));
       slack = std::max(slack, std::fabs((double)hi - (double)plane[2 * j + 1]));
     }
-    if (!(ilo <= ihi)) return false;
-    inner[2 * j] = ilo;
-    inner[2 * j + 1] = ihi;
   }
   if (!(B > 0) || !(B <= 0x1p100) || !(slack <= 0x1p-20 * B)) return false;
   std::copy(plane, plane + 6, out);
-  std::copy(inner, inner + 6, out + 6);
   mB = std::nextafter((float)(0x1p-21 * B + slack), INFINITY);
   return true;
 }
@@ -641,19 +632,16 @@ struct Flattener {
     const Obj& o = s.objs[(size_t)i];
     return inside(o.aabb) && inside(s.objs[(size_t)o.child].aabb) && inside(s.objs[(size_t)s.root].aabb);
   }
-  // Box-level steps (boxaa.h) for scenes with spheres: their kernels (render.hip BoxOn) take them; the
-  // sphere-free kernels (the Cornell boxes) run the six-face runs, which measured cheaper there (DESIGN.md
-  // §4 "Box-level test"). RT2_BOX_AA=0 keeps every MakeBox a plain run, 1 forces the steps (tests).
-  bool box_aa = false;
+  // Box-level steps (boxaa.h) for every MakeBox run whose faces take the QUADAA test (DESIGN.md §4
+  // "Box-level test"). RT2_BOX_AA=0 keeps every MakeBox a plain six-face run (the A/B baseline).
+  bool box_aa = true;
   std::vector<uint32_t> box_runs;  // first quad step of each MakeBox run with a box record
   void SetBoxAA() {
-    bool spheres = false;
-    for (const Obj& o : s.objs) spheres = spheres || o.kind == kSphere;
-    box_aa = spheres;
-    if (const char* e = getenv("RT2_BOX_AA")) box_aa = atoi(e) != 0 && (spheres || atoi(e) == 2);
+    const char* e = getenv("RT2_BOX_AA");
+    box_aa = !(e && atoi(e) == 0);
   }
   // A list that is a MakeBox whose faces all take the QUADAA rectangle test in this space: its box words
-  bool BoxList(const Obj& o, uint32_t parent_xf, const std::vector<float>& lind, float bw[12], float& mB) const {
+  bool BoxList(const Obj& o, uint32_t parent_xf, const std::vector<float>& lind, float bw[6], float& mB) const {
     if (o.kind != kList || o.children.size() != 6 || !QuadAASpace(parent_xf, lind)) return false;
     const float* faces[6];
     for (int j = 0; j < 6; j++) {
@@ -711,16 +699,16 @@ struct Flattener {
         }
         {
           // a MakeBox list (Quad.hpp:34-50) whose six faces take the QUADAA test: its box record (boxaa.h:
-          // 12 words, then mB, padded to 4 records) right before the faces' records, and its first quad
+          // the six planes, then mB, padded to 2 records) right before the faces' records, and its first quad
           // step noted; after the run pass its run (exactly these six quads) gets the box flag (aux bit
           // 31), and the kernel runs the box-level test before the six-face run
           if (box_aa) {
-            float bw[12], mB;
+            float bw[6], mB;
             if (BoxList(o, parent_xf, lind, bw, mB)) {
-              float rec[16] = {};
-              std::copy(bw, bw + 12, rec);
-              rec[12] = mB;
-              lind.insert(lind.end(), rec, rec + 16);
+              float rec[4 * kBoxAARecords] = {};
+              std::copy(bw, bw + 6, rec);
+              rec[6] = mB;
+              lind.insert(lind.end(), rec, rec + 4 * kBoxAARecords);
               box_runs.push_back((uint32_t)(lin.size() / 4));
             }
           }
@@ -870,7 +858,7 @@ void PackTextures(const Scene& s, CompiledScene& out) {
 }  // namespace
 
 bool QuadAATestWords(const float* r, int k, float out[8]) { return RectAAWords(r, k, out); }
-bool BoxAAWords(const float* const faces[6], float out[12], float& mB) { return BoxAAWordsOf(faces, out, mB); }
+bool BoxAAWords(const float* const faces[6], float out[6], float& mB) { return BoxAAWordsOf(faces, out, mB); }
 
 bool CompileScene(const Scene& s, CompiledScene& out, std::string& err, bool accelerate_lists) {
   return CompileSceneWith(s, out, err, accelerate_lists, kAccDepthSlack);

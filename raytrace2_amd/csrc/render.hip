@@ -863,6 +863,17 @@ struct BoxMath {
   static __device__ __forceinline__ float max(float a, float b) { return vmax(a, b); }
   static __device__ __forceinline__ float min3(float a, float b, float c) { return vmin3(a, b, c); }
   static __device__ __forceinline__ float max3(float a, float b, float c) { return vmax3(a, b, c); }
+  // min / max of the magnitudes, the |.| as source modifiers
+  static __device__ __forceinline__ float amin3(float a, float b, float c) {
+    float r;
+    asm("v_min3_f32 %0, |%1|, |%2|, |%3|" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+  }
+  static __device__ __forceinline__ float amax3(float a, float b, float c) {
+    float r;
+    asm("v_max3_f32 %0, |%1|, |%2|, |%3|" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+  }
   static __device__ __forceinline__ float med3(float a, float b, float c) { return __builtin_amdgcn_fmed3f(a, b, c); }
   static __device__ __forceinline__ float fma(float a, float b, float c) { return fmaf(a, b, c); }
   static __device__ __forceinline__ float abs(float a) { return fabsf(a); }
@@ -1510,12 +1521,11 @@ __device__ __forceinline__ uint32_t wave_min_next(uint32_t next) {
   return i;
 }
 
-// The box-level test of box-flagged MakeBox runs runs in the sphere kernels (the compiler flags runs only
-// in scenes with spheres: book 2's ground boxes; the Cornell box kernel measured its two boxes' runs cheaper
-// than the test, DESIGN.md §4 "Box-level test").
+// The box-level test of box-flagged MakeBox runs (boxaa.h), in every kernel with quads (the compiler flags
+// the runs: book 2's ground boxes, the Cornell box's two boxes; DESIGN.md §4 "Box-level test").
 template <uint32_t F>
 constexpr bool BoxOn() {
-  return Has<F, kFeatSphere>();
+  return true;
 }
 template <uint32_t F, bool kStats, class W, class G>
 __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wray, float time, G& path, HitRef& h,
@@ -1607,19 +1617,19 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
       const uint32_t run = st.w & kRunLenMask;
       // A MakeBox run with a box record (aux bit 31; compile.cpp, for scenes with spheres): the box-level
       // test (boxaa.h) first. A certified lane takes the candidate face's answer and skips the run; the
-      // wave runs the six faces only for the lanes it could not certify. The box record (12 words) lies
-      // right before the run's first face record; aux = run | flag, the margin constant in the record's
-      // trailing word (compile.cpp BoxAAWordsOf).
+      // wave runs the six faces only for the lanes it could not certify. The box record (six planes and
+      // the margin constant, 2 records) lies right before the run's first face record; aux = run | flag
+      // (compile.cpp BoxAAWordsOf).
       bool boxed = false;
       if constexpr (BoxOn<F>()) {
         if ((int)st.w < 0) {
-          const u32x16 bwr = sld16(recs, (off - 4u) * 16u);
+          const u32x8 bwr = sld8(recs, (off - (uint32_t)kBoxAARecords) * 16u);
           float bw[kBoxAAWords];
 #pragma unroll
           for (int j = 0; j < kBoxAAWords; j++) bw[j] = uf(bwr[j]);
           const uint32_t kmax0 = bits(tmax) - bits(tmin);
           const BoxAAResult r =
-              BoxAATest<BoxMath>(bw, uf(bwr[12]), o.x, o.y, o.z, d.x, d.y, d.z, inv.x, inv.y, inv.z, tmin, kmax0);
+              BoxAATest<BoxMath>(bw, uf(bwr[6]), o.x, o.y, o.z, d.x, d.y, d.z, inv.x, inv.y, inv.z, tmin);
           if (kStats) {
             cnt.box++;
             const bool lead = (int)__lane_id() == __builtin_amdgcn_readfirstlane((int)__lane_id());

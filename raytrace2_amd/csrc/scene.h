@@ -168,10 +168,10 @@ bool CompileSceneWith(const Scene& s, CompiledScene& out, std::string& err, bool
 // The 8 QUADAA test words of QUAD record r (20 floats, rt2_layout.h) with axis code k + 4, or false when
 // the quad takes the general path (compile.cpp RectAAWords; for tests/cpp/quadaa_bounds.cpp).
 bool QuadAATestWords(const float* r, int k, float out[8]);
-// The box step's 12 record words and margin constant (boxaa.h) of six QUAD records in MakeBox order, or
+// The box record's six planes and margin constant (boxaa.h) of six QUAD records in MakeBox order, or
 // false when they are not a box the box-level test can take (compile.cpp BoxAAWordsOf; for
 // tests/cpp/box_cert.cpp).
-bool BoxAAWords(const float* const faces[6], float out[12], float& mB);
+bool BoxAAWords(const float* const faces[6], float out[6], float& mB);
 
 // Philox4x32-10 (shared constants with the kernel; see render.hip)
 void Philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1);

@@ -48,6 +48,8 @@ struct HostMath {
   static float max(float a, float b) { return std::fmax(a, b); }
   static float min3(float a, float b, float c) { return std::fmin(std::fmin(a, b), c); }
   static float max3(float a, float b, float c) { return std::fmax(std::fmax(a, b), c); }
+  static float amin3(float a, float b, float c) { return min3(std::fabs(a), std::fabs(b), std::fabs(c)); }
+  static float amax3(float a, float b, float c) { return max3(std::fabs(a), std::fabs(b), std::fabs(c)); }
   static float med3(float a, float b, float c) { return std::fmax(std::fmin(a, b), std::fmin(std::fmax(a, b), c)); }
   static float fma(float a, float b, float c) { return std::fma(a, b, c); }
   static float abs(float a) { return std::fabs(a); }
@@ -56,7 +58,7 @@ struct HostMath {
 constexpr float kAbove1e8 = 0x1.5798f0p-27f;
 
 struct Box {
-  float w[12];
+  float w[kBoxAAWords];
   float mB;
   float tw[6][8];  // the run's QUADAA test words
   int axis[6];
@@ -129,7 +131,7 @@ int main(int argc, char** argv) {
   Scene s;
   std::string err;
   CompiledScene c;
-  setenv("RT2_BOX_AA", "2", 1);  // box steps in a sphere-free scene too (compile.cpp SetBoxAA)
+  unsetenv("RT2_BOX_AA");  // the default: box steps (compile.cpp SetBoxAA)
   if (!LoadScene(path, 1, s, err) || !CompileScene(s, c, err)) {
     fprintf(stderr, "scene: %s\n", err.c_str());
     return 2;
@@ -143,9 +145,9 @@ int main(int argc, char** argv) {
       fprintf(stderr, "box run at step %zu is not a MakeBox run\n", i);
       return 1;
     }
-    const size_t rec = c.lin[4 * i + 2];  // the run's first face record; the box record is the 4 before it
-    memcpy(bx.w, &c.lind[4 * (rec - 4)], 48);
-    bx.mB = c.lind[4 * (rec - 4) + 12];
+    const size_t rec = c.lin[4 * i + 2];  // the run's first face record; the box record is the 2 before it
+    memcpy(bx.w, &c.lind[4 * (rec - kBoxAARecords)], 4 * kBoxAAWords);
+    bx.mB = c.lind[4 * (rec - kBoxAARecords) + 6];
     for (int j = 0; j < 6; j++) {
       if (c.lin[4 * (i + j) + 2] != rec + 5u * (uint32_t)j) {
         fprintf(stderr, "box run at step %zu: face records are not contiguous\n", i);
@@ -240,8 +242,8 @@ int main(int argc, char** argv) {
       uint32_t kmax = kmax0;
       int prim = -1;
       Run(bx, o, d, inv, tmin, kmax, prim);
-      const BoxAAResult res = BoxAATest<HostMath>(bx.w, bx.mB, o[0], o[1], o[2], d[0], d[1], d[2], inv[0], inv[1], inv[2],
-                                                  tmin, kmax0);
+      const BoxAAResult res =
+          BoxAATest<HostMath>(bx.w, bx.mB, o[0], o[1], o[2], d[0], d[1], d[2], inv[0], inv[1], inv[2], tmin);
       tot[cls]++;
       if (prim >= 0) hits[cls]++;
       if (!res.cert) continue;

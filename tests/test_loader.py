@@ -60,7 +60,7 @@ def test_scene_compile_facts():
     assert b2.linear_steps == 4922 + 7 * 1999
     assert b2.max_stack <= 24
     assert info.acc_lists == 0 and info.linear_steps > 0
-    assert info.box_steps == 0  # sphere-free scenes keep the six-face runs (render.hip BoxOn)
+    assert info.box_steps == 2  # the Cornell box's two boxes (in their transforms' model space)
 
 
 @pytest.mark.parametrize("name,bounded", [("cornell_box_original", 1), ("cornell_box_volume", 1),
