@@ -19,9 +19,10 @@ VOL="--scene cornell_box_volume.json --spp 4000"
 B2="--scene book2_final_scene_10000_samples.json --width 800 --height 800 --spp 10000"
 run "C1 cornell 400^2 @ 64" --width 400 --height 400 --spp 64 --steps 5
 run "C2 cornell 1024^2 @ 1000" --steps 3
-run "C2 8-way, every rank" --steps 2 --emulate-world 8 --emulate-rank all
-run "C2 4-way, every rank" --steps 2 --emulate-world 4 --emulate-rank all
-run "C2 2-way, every rank" --steps 2 --emulate-world 2 --emulate-rank all
+# (a rank's step is a 20-40 ms launch: 10 steps after 2 warm-up ones, as the driver's runs do many)
+run "C2 8-way, every rank" --steps 10 --warmup 2 --emulate-world 8 --emulate-rank all
+run "C2 4-way, every rank" --steps 10 --warmup 2 --emulate-world 4 --emulate-rank all
+run "C2 2-way, every rank" --steps 5 --warmup 2 --emulate-world 2 --emulate-rank all
 run "C3 book1 1920x1080 @ 500" $B1 --steps 2
 run "C4 cornell volume 1024^2 @ 4000" $VOL
 run "C4 8-way, every rank" $VOL --emulate-world 8 --emulate-rank all --warmup 0
