@@ -55,8 +55,7 @@ constexpr int kBlock = 256;
                          // 16 quad-run test, 32 threaded medium step, 64 its log, 128 its two boundary
                          // queries, 256 a Philox block (at every refill), 512 the sample store /
                          // staging, 2048 a threaded transform entry (ray into model space, its reciprocal),
-                         // 4096 an accelerated list's lane walk, 8192 a box-level test of a MakeBox run
-                         // beside the run (what one candidate face + a certificate costs)
+                         // 4096 an accelerated list's lane walk
 #endif
 #ifndef RT2_EXP_WAVESTEPS
 #define RT2_EXP_WAVESTEPS 0  // diagnostic build: per-wave linear-traversal step counts into diag slots
@@ -1659,53 +1658,6 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
       // instructions and a copy to build each accepted ref: the scalar unit is the busier pipe)
       uint32_t vref = make_ref(kQuadAA, off);
       asm volatile("" : "+v"(vref));
-#if RT2_EXP_TWICE & 8192
-      // Cost probe (result discarded): the box-level test of a MakeBox run (6 QUADAA faces in the
-      // order z+ x+ z- x- y+ y-, Quad.hpp:43-48): every plane's exact t (the value each face's own test
-      // computes), the slab classification (entry / exit, second nearest), the candidate face's hit
-      // point and interior test against an inner and an outer box (a face-independent answer unless
-      // the point lies in the few-ulp shell between them), the certificate's coordinate gaps and
-      // margin, and the candidate's key. The instruction count this adds is the cost of the test the
-      // real implementation would run instead of the six-face run (DESIGN.md §4 "Box-level test").
-      if (run == 6u && st.y == 01554646u) {
-        // a compact box record as the compiler would lay it out: 16 words (two faces' test words:
-        // z+ plane, x/y bounds; x+ plane, y/z bounds) + the other four planes
-        const u32x16 fb = sld16(recs, off * 16u);
-        const uint32_t pz2 = sld1(recs, off * 16u + 2u * 16u * (uint32_t)kQuadRecords);
-        const uint32_t px3 = sld1(recs, off * 16u + 3u * 16u * (uint32_t)kQuadRecords);
-        const uint32_t py4 = sld1(recs, off * 16u + 4u * 16u * (uint32_t)kQuadRecords);
-        const uint32_t py5 = sld1(recs, off * 16u + 5u * 16u * (uint32_t)kQuadRecords);
-        f3 o2 = o;
-        asm volatile("" : "+v"(o2.x), "+v"(o2.y), "+v"(o2.z));
-        const float tz0 = div_by_inv(uf(fb[0]) - o2.z, d.z, inv.z), tx1 = div_by_inv(uf(fb[8]) - o2.x, d.x, inv.x);
-        const float tz2 = div_by_inv(uf(pz2) - o2.z, d.z, inv.z), tx3 = div_by_inv(uf(px3) - o2.x, d.x, inv.x);
-        const float ty4 = div_by_inv(uf(py4) - o2.y, d.y, inv.y), ty5 = div_by_inv(uf(py5) - o2.y, d.y, inv.y);
-        const float tnx = vmin(tx1, tx3), tfx = vmax(tx1, tx3), tny = vmin(ty4, ty5), tfy = vmax(ty4, ty5);
-        const float tnz = vmin(tz0, tz2), tfz = vmax(tz0, tz2);
-        const float tin = vmax3(tnx, tny, tnz), tout = vmin3(tfx, tfy, tfz);
-        const float t2 = __builtin_amdgcn_fmed3f(tnx, tny, tnz), x2 = __builtin_amdgcn_fmed3f(tfx, tfy, tfz);
-        const bool ex = tin == tnx, ey = tin == tny, xx = tout == tfx, xy = tout == tfy;
-        const bool nearc = tin >= tmin;
-        const float tc = nearc ? tin : tout;
-        const bool kx = nearc ? ex : xx, ky = nearc ? ey : xy;
-        const float px = o2.x + d.x * tc, py = o2.y + d.y * tc, pz = o2.z + d.z * tc;
-        // inner bounds: the two faces' words; outer: the same widened (the compiler's outer box)
-        const float qx = kx ? uf(fb[1]) : px, qy = ky ? uf(fb[3]) : py, qz = (!kx && !ky) ? uf(fb[11]) : pz;
-        const uint32_t win = (bits(qx - uf(fb[1])) | bits(uf(fb[2]) - qx) | bits(qy - uf(fb[3]))) |
-                             (bits(uf(fb[4]) - qy) | bits(qz - uf(fb[11])) | bits(uf(fb[12]) - qz));
-        const uint32_t wout = (bits(qx - uf(fb[9])) | bits(uf(fb[10]) - qx) | bits(qy - uf(fb[5]))) |
-                              (bits(uf(fb[6]) - qy) | bits(qz - uf(fb[13])) | bits(uf(fb[14]) - qz));
-        const float ade = ex ? fabsf(d.x) : (ey ? fabsf(d.y) : fabsf(d.z));
-        const float adx = xx ? fabsf(d.x) : (xy ? fabsf(d.y) : fabsf(d.z));
-        const float m = 0x1p-19f * (vmax3(fabsf(o2.x), fabsf(o2.y), fabsf(o2.z)) +
-                                    fabsf(tc) * vmax3(fabsf(d.x), fabsf(d.y), fabsf(d.z)) + uf(fb[7]));
-        const bool cert = nearc ? (tin < tout ? ade * (tin - t2) >= m : vmin(ade, adx) * (tin - tout) >= 2.0f * m)
-                                : adx * (x2 - tout) >= m;
-        const uint32_t key = (bits(tc) - bits(tmin)) | (win & 0x80000000u);
-        const bool amb = (int)win < 0 && (int)wout >= 0;
-        asm volatile("" ::"v"(key), "v"((int)(cert && !amb)));
-      }
-#endif
       for (bool first = true;; first = false) {
         const uint32_t c0 = codes & 7u;
         float t0;

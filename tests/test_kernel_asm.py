@@ -120,7 +120,7 @@ def test_book2_trace_loops_keep_the_scalar_issue_code_generation(isa):
     the depth-3 loop with a scalar record load and v_or3 rejection words) holds three separate QUADAA
     interior tests (6 v_or3), no exec-mask save per quad and at most 28 SALU (23); its BVH-step loop at
     most 32 SALU (27); its trace loop, which holds the box-level test of flagged MakeBox runs (boxaa.h), at
-    most 440 SALU (409; 361 before the box test; 586 without -structurizecfg-skip-uniform-regions, and
+    most 440 SALU (377; 361 before the box test; 586 without -structurizecfg-skip-uniform-regions, and
     without -simplifycfg-sink-common=false the quad bodies merge into one: 2 v_or3)."""
     _, body = _kernel(isa, "ILj815ELi2ELb0E")
     loops = _loops(body)
@@ -183,7 +183,8 @@ def test_cornell_quad_run_loop_keeps_the_scalar_issue_code_generation(isa):
     with a scalar record load whose QUADAA test ORs its rejection words with v_or3, two per axis body)
     must hold three separate interior tests (6 v_or3; one merged body: 2), no exec-mask save per quad,
     and at most 28 SALU instructions (with the options: 22; without them: one merged body, 12 SALU but
-    every axis's copies); its trace loop at most 150 SALU (124; without: 205)."""
+    every axis's copies); its trace loop at most 150 SALU (140 with the box-level test of the boxes'
+    MakeBox runs, 124 before it; without the options: 205)."""
     _, body = _kernel(isa, "ILj4ELi2ELb0E")
     loops = _loops(body)
     quad = [(h, c) for h, d, c in loops if d == 3 and c["v_or3_b32"] > 0 and any(k.startswith("s_load") for k in c)]
