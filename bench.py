@@ -53,7 +53,8 @@ REC_BYTES = {"bvh_tests": 32, "quad_tests": 80, "sphere_tests": 32, "xform_visit
              "list_visits": 16}
 FLOPS = {"bvh_tests": 18, "quad_tests": 45, "sphere_tests": 30, "xform_visits": 45, "medium_tests": 20}
 GATHER_REPS = 5  # isolated gathers timed after the steps (gather_ms_per_step)
-KERNEL_SOURCES = ["raytrace2_amd/csrc/render.hip", "raytrace2_amd/csrc/rt2_layout.h", "raytrace2_amd/csrc/Makefile"]
+KERNEL_SOURCES = ["raytrace2_amd/csrc/render.hip", "raytrace2_amd/csrc/rt2_layout.h", "raytrace2_amd/csrc/boxaa.h",
+                  "raytrace2_amd/csrc/Makefile"]
 
 
 def kernel_sha() -> str:
