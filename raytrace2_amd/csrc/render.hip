@@ -55,7 +55,7 @@ constexpr int kBlock = 256;
                          // 16 quad-run test, 32 threaded medium step, 64 its log, 128 its two boundary
                          // queries, 256 a Philox block (at every refill), 512 the sample store /
                          // staging, 2048 a threaded transform entry (ray into model space, its reciprocal),
-                         // 4096 an accelerated list's lane walk
+                         // 4096 an accelerated list's lane walk, 8192 the box-level test of a MakeBox run
 #endif
 #ifndef RT2_EXP_WAVESTEPS
 #define RT2_EXP_WAVESTEPS 0  // diagnostic build: per-wave linear-traversal step counts into diag slots
@@ -1629,6 +1629,15 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
           const uint32_t kmax0 = bits(tmax) - bits(tmin);
           const BoxAAResult r =
               BoxAATest<BoxMath>(bw, uf(bwr[6]), o.x, o.y, o.z, d.x, d.y, d.z, inv.x, inv.y, inv.z, tmin);
+#if RT2_EXP_TWICE & 8192
+          {
+            float ox2 = o.x;
+            asm volatile("" : "+v"(ox2));
+            const BoxAAResult r2 =
+                BoxAATest<BoxMath>(bw, uf(bwr[6]), ox2, o.y, o.z, d.x, d.y, d.z, inv.x, inv.y, inv.z, tmin);
+            asm volatile("" ::"v"(r2.x), "v"(r2.t), "v"(r2.face), "v"((int)r2.cert));
+          }
+#endif
           if (kStats) {
             cnt.box++;
             const bool lead = (int)__lane_id() == __builtin_amdgcn_readfirstlane((int)__lane_id());

@@ -197,7 +197,7 @@ def test_cornell_quad_run_loop_keeps_the_scalar_issue_code_generation(isa):
     assert len(trace) == 1 and _salu(trace[0]) <= 150, [_salu(c) for c in trace]
 
 
-@pytest.mark.parametrize("define", ["RT2_EXP_TRACE_TWICE=1", "RT2_EXP_TWICE=8191", "RT2_EXP_WAVESTEPS=1",
+@pytest.mark.parametrize("define", ["RT2_EXP_TRACE_TWICE=1", "RT2_EXP_TWICE=16383", "RT2_EXP_WAVESTEPS=1",
                                     "RT2_EXP_STAMPS=1", "RT2_EXP_ENDTIME=1", "RT2_EXP_NOSTORE=1"])
 def test_diagnostic_builds_compile(define, tmp_path):
     """The only #if sides left in render.hip are the tools/ diagnostic builds (cost probes, wave-step
