@@ -62,7 +62,7 @@ typedef struct {
   int origins_bounded;      /* 1: the threaded program's exact tests need camera rays starting within
                              * +-2^64 (rectangle quads, box boundaries, transforms about y); a launch
                              * refuses a camera beyond that (RT2_ERR_INVALID). 0: any camera renders */
-  int box_steps;            /* MakeBox runs given a box-level test step in the threaded program */
+  int box_steps;            /* MakeBox runs and MakeBox medium boundaries given the box-level test */
 } rt2_scene_info;
 RT2_API int rt2_scene_get_info(const rt2_scene* scene, rt2_scene_info* out);
 /* Material table, 8 floats per material: type, albedo.xyz, fuzz, refraction_index, tex_idx, 0.

@@ -87,4 +87,40 @@ RT2_BOXAA_FN BoxAAResult BoxAATest(const float* w, float mB, float ox, float oy,
   return r;
 }
 
+// Both boundary queries of ConstantMedium::Hit on a MakeBox boundary (ConstantMedium.cpp:14-58; render.hip
+// boundary_aa_pair: t1 = the smallest accepted face t in [-FLT_MAX, FLT_MAX], t2 = the smallest in
+// [fl(t1 + 0.0001), FLT_MAX]). Under the certificate dmin * min(T_in - T2, X2 - T_out, |T_out - T_in| / 2)
+// >= m (both side gaps: the entry and the exit face are both candidates), a line through the box has
+// exactly two accepting faces, the entry face at T_in and the exit face at T_out (each one's point lies
+// inside every other slab, every other face's point outside a slab), and a line past it none. The
+// queries' intervals do not enter: every other face is rejected by its interior test.
+struct BoxAAPairResult {
+  bool cert;  // the two faces below are the boundary's only accepting faces (none when !through)
+  bool through;
+  float tin, tout;
+};
+template <class M>
+RT2_BOXAA_FN BoxAAPairResult BoxAAPair(const float* w, float mB, float ox, float oy, float oz, float dx, float dy,
+                                       float dz, float ix, float iy, float iz) {
+  const float ax = M::div(w[0] - ox, dx, ix), bx = M::div(w[1] - ox, dx, ix);
+  const float ay = M::div(w[2] - oy, dy, iy), by = M::div(w[3] - oy, dy, iy);
+  const float az = M::div(w[4] - oz, dz, iz), bz = M::div(w[5] - oz, dz, iz);
+  const float tnx = M::min(ax, bx), tfx = M::max(ax, bx);
+  const float tny = M::min(ay, by), tfy = M::max(ay, by);
+  const float tnz = M::min(az, bz), tfz = M::max(az, bz);
+  const float tin = M::max3(tnx, tny, tnz), tout = M::min3(tfx, tfy, tfz);
+  const float t2 = M::med3(tnx, tny, tnz), x2 = M::med3(tfx, tfy, tfz);
+  const float dmin = M::amin3(dx, dy, dz), dmax = M::amax3(dx, dy, dz);
+  const float tabs = M::amax3(M::amax3(tin, t2, tout), x2, x2);
+  const float omax = M::amax3(ox, oy, oz);
+  const float m = M::fma(0x1p-21f, M::fma(dmax, tabs, omax), mB);
+  const float g = M::min(M::min(tin - t2, x2 - tout), 0.5f * M::abs(tout - tin));
+  BoxAAPairResult r;
+  r.cert = (dmin >= kBoxAADenomMin) & (dmin * g >= m);
+  r.through = tin < tout;
+  r.tin = tin;
+  r.tout = tout;
+  return r;
+}
+
 }  // namespace rt2

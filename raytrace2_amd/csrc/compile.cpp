@@ -554,7 +554,21 @@ struct Flattener {
     }
     lind.insert(lind.end(), words.begin(), words.end());
     origins_bounded = true;
-    return kBoundaryAAFlag | ((uint32_t)o.children.size() << 24) | codes;
+    uint32_t box = 0;
+    if (box_aa && o.children.size() == 6) {  // a MakeBox: its box record (boxaa.h BoxAAPair) follows
+      const float* faces[6];
+      for (int j = 0; j < 6; j++) faces[j] = out.nodes.data() + 4 * (size_t)(ref_of.at(o.children[(size_t)j]) & kOffsetMask);
+      float bw[6], mB;
+      if (BoxAAWordsOf(faces, bw, mB)) {
+        float rec[4 * kBoxAARecords] = {};
+        std::copy(bw, bw + 6, rec);
+        rec[6] = mB;
+        lind.insert(lind.end(), rec, rec + 4 * kBoxAARecords);
+        box = kBoundaryBoxFlag;
+        out.box_steps++;
+      }
+    }
+    return kBoundaryAAFlag | box | ((uint32_t)o.children.size() << 24) | codes;
   }
   // An accelerated list's tree in the threaded program: ACCBVH steps (padded box, skip = index
   // after the subtree) near child first, ACCSPHERE steps with aux = the sphere's record offset in

@@ -1294,15 +1294,36 @@ __device__ __forceinline__ bool boundary_aa_pair(const void* recs, uint32_t off,
 
 // medium_t with the boundary queries above (same operations, same random draw)
 template <uint32_t F, class G>
-__device__ __forceinline__ bool medium_t_lin(const void* recs, uint32_t moff, const u32x4 r0, f3 o, f3 d, float time,
-                                             float tmin, float tmax, G& path, lds_u32* cand, float& t_out,
+__device__ __forceinline__ bool medium_t_lin(const void* recs, uint32_t moff, const u32x4 r0, f3 o, f3 d, f3 inv,
+                                             float time, float tmin, float tmax, G& path, lds_u32* cand, float& t_out,
                                              Counters& cnt) {
   const uint32_t bref = r0.z;
   float t1, t2;
   // a box (the sphere scenes' kernels keep the general path: the 48 words cost them SGPRs)
   if (!Has<F, kFeatSphere>() && (r0.w & kBoundaryAAFlag)) {
     const uint32_t off = (moff + 1u) * 16u;
-    if (!boundary_aa_pair(recs, off, r0.w, o, d, t1, t2, cand, cnt)) return false;
+    // a MakeBox boundary: the box-level test of both queries (boxaa.h BoxAAPair); the lanes it cannot
+    // certify take the six faces
+    bool cert = false, ok = false;
+    if (r0.w & kBoundaryBoxFlag) {
+      const u32x8 bwr = sld8(recs, off + 32u * kBoundaryAAMax);
+      float bw[kBoxAAWords];
+#pragma unroll
+      for (int j = 0; j < kBoxAAWords; j++) bw[j] = uf(bwr[j]);
+      const BoxAAPairResult r = BoxAAPair<BoxMath>(bw, uf(bwr[6]), o.x, o.y, o.z, d.x, d.y, d.z, inv.x, inv.y, inv.z);
+      if (r.cert) {
+        cert = true;
+        cnt.quad += 2u * kBoundaryAAMax;  // the two queries' face tests (the reference's count)
+        // the second query's interval starts at fl(t1 + 0.0001): t1 itself for a large t1 (its face
+        // then answers both queries), else past it (the exit face answers)
+        const float lb = (float)((double)r.tin + 0.0001);
+        t1 = r.tin;
+        t2 = lb <= r.tin ? r.tin : r.tout;
+        ok = r.through && t2 >= lb;
+      }
+    }
+    if (!cert) ok = boundary_aa_pair(recs, off, r0.w, o, d, t1, t2, cand, cnt);
+    if (!ok) return false;
   } else {
 #if RT2_EXP_TWICE & 128
   {
@@ -1906,11 +1927,11 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
         G p2 = path;
         Counters c2 = cnt;
         float t2 = 0.0f;
-        const bool h2 = medium_t_lin<F>(recs, off, mr, o2, d, time, tmin, tmax, p2, cand, t2, c2);
+        const bool h2 = medium_t_lin<F>(recs, off, mr, o2, d, inv, time, tmin, tmax, p2, cand, t2, c2);
         asm volatile("" ::"v"(t2), "v"((int)h2));
       }
 #endif
-      if (medium_t_lin<F>(recs, off, mr, o, d, time, tmin, tmax, path, cand, t, cnt)) {
+      if (medium_t_lin<F>(recs, off, mr, o, d, inv, time, tmin, tmax, path, cand, t, cnt)) {
         tmax = t;
         prim = make_ref(kMedium, off);
         h.xf = cur_xf;

@@ -90,7 +90,8 @@ inline constexpr uint32_t make_ref(uint32_t kind, uint32_t off) { return (kind <
 //          kBoundaryAAMax unit-normal axis-aligned quads (a box in the medium's space) also has its
 //          children's 8-word QUADAA test records right after the medium record, and word 3 =
 //          kBoundaryAAFlag | count << 24 | (axis K of child k) << 3k (boundary_ref keeps the
-//          general copy).
+//          general copy); a MakeBox boundary (six faces, boxaa.h BoxAAWords) also has
+//          kBoundaryBoxFlag and its 2-record box record (six planes, margin) after the quads' words.
 //  LISTACC: (center.xyz, R) (k2, k1, k0, root_ref bits): a HittableList of n >= kListAccelMin
 //          spheres (HittableList.cpp:8-22). The list returns the smallest accepted root and, on
 //          equal roots, its first child (Sphere uses the strict Surrounds), so any visiting
@@ -117,6 +118,7 @@ inline constexpr float acc_slab_inv(float inv) {
   return inv > 0x1p100f ? 0x1p100f : (inv < -0x1p100f ? -0x1p100f : inv);
 }
 constexpr uint32_t kBoundaryAAFlag = 0x80000000u;
+constexpr uint32_t kBoundaryBoxFlag = 0x08000000u;  // a MakeBox boundary: a box record (boxaa.h) follows
 constexpr uint32_t kBoundaryAAMax = 6;
 
 constexpr int kBvhRecords = 2, kQuadRecords = 5, kSphereRecords = 2, kXformRecords = 8, kMediumRecords = 1;

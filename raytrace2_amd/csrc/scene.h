@@ -145,7 +145,7 @@ struct CompiledScene {
   int lin_xform_depth = 0;        // deepest transform nesting in the threaded program (0: none)
   int bvh_nodes = 0, quads = 0, spheres = 0, lists = 0, xforms = 0, media = 0;
   int acc_lists = 0, acc_nodes = 0;  // exact list acceleration trees (rt2_layout.h LISTACC)
-  int box_steps = 0;                 // MakeBox runs given a box record and the box-level test (boxaa.h)
+  int box_steps = 0;                 // MakeBox runs and medium boundaries given a box record (boxaa.h)
   int bvh_depth = 0;
   uint32_t features = 0;          // rt2_layout.h Feature bits (defocus is added per render)
   // The threaded program uses a test that is exact only for ray origins within +-2^64 in world space

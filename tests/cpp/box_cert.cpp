@@ -78,6 +78,30 @@ void Run(const Box& bx, const float o[3], const float d[3], const float inv[3], 
   }
 }
 
+// both boundary queries of ConstantMedium::Hit on the box as render.hip boundary_aa_pair runs them: each
+// face's t by IEEE division and its QUADAA interior test (quad_aa_div), candidates in [-FLT_MAX,
+// FLT_MAX]; t1 = the smallest, t2 = the smallest >= fl(t1 + 0.0001)
+bool Pair(const Box& bx, const float o[3], const float d[3], float& t1, float& t2) {
+  float c[6], m = INFINITY;
+  for (int j = 0; j < 6; j++) {
+    const int k = bx.axis[j], a = (k + 1) % 3, b = (k + 2) % 3;
+    const float* r = bx.tw[j];
+    const float t = (r[0] - o[k]) / d[k];
+    const float pa = o[a] + d[a] * t, pb = o[b] + d[b] * t;
+    const uint32_t rej = (B(pa - r[1]) | B(r[2] - pa) | B(pb - r[3])) | (B(r[4] - pb) | B(std::fabs(d[k]) - kAbove1e8));
+    c[j] = ((int32_t)rej >= 0 && -FLT_MAX <= t && t <= FLT_MAX) ? t : INFINITY;
+    m = std::fmin(m, c[j]);
+  }
+  if (!(m <= FLT_MAX)) return false;
+  t1 = m;
+  const float lb = (float)((double)m + 0.0001);
+  float m2 = INFINITY;
+  for (int j = 0; j < 6; j++) m2 = (lb <= c[j] && c[j] < m2) ? c[j] : m2;
+  if (!(m2 <= FLT_MAX)) return false;
+  t2 = m2;
+  return true;
+}
+
 std::mt19937_64 rng;
 float U(float lo, float hi) { return std::uniform_real_distribution<float>(lo, hi)(rng); }
 float Ulps(float x, int n) {  // x moved by n ulps
@@ -163,7 +187,7 @@ int main(int argc, char** argv) {
     return 1;
   }
   const char* names[] = {"enter face", "enter edge/corner", "graze", "leave surface", "inside", "near miss", "zero comp"};
-  long tot[7] = {}, cert[7] = {}, hits[7] = {};
+  long tot[7] = {}, cert[7] = {}, hits[7] = {}, pcert[7] = {};
   const float tmin = 0.001f;
   for (const Box& bx : boxes) {
     const float lo[3] = {bx.w[0], bx.w[2], bx.w[4]}, hi[3] = {bx.w[1], bx.w[3], bx.w[5]};
@@ -244,6 +268,26 @@ int main(int argc, char** argv) {
       Run(bx, o, d, inv, tmin, kmax, prim);
       const BoxAAResult res =
           BoxAATest<HostMath>(bx.w, bx.mB, o[0], o[1], o[2], d[0], d[1], d[2], inv[0], inv[1], inv[2], tmin);
+      // the medium form: both boundary queries (boxaa.h BoxAAPair)
+      {
+        float q1 = 0, q2 = 0;
+        const bool qok = Pair(bx, o, d, q1, q2);
+        const BoxAAPairResult pr =
+            BoxAAPair<HostMath>(bx.w, bx.mB, o[0], o[1], o[2], d[0], d[1], d[2], inv[0], inv[1], inv[2]);
+        if (pr.cert) {
+          pcert[cls]++;
+          // the second query starts at fl(t1 + 0.0001), which is t1 itself for a t1 above 2^10 or so
+          const float lb = (float)((double)pr.tin + 0.0001);
+          const float bt2 = lb <= pr.tin ? pr.tin : pr.tout;
+          const bool bok = pr.through && bt2 >= lb;
+          // (t values compared as values: a +-0 t1 is clamped to tmin by the medium step either way)
+          if (bok != qok || (qok && (q1 != pr.tin || q2 != bt2 || (q1 != 0.0f && B(q1) != B(pr.tin))))) {
+            fprintf(stderr, "PAIR MISMATCH class %s: queries %d t1 %a t2 %a, box %d t1 %a t2 %a\n o = (%a %a %a) d = (%a %a %a)\n",
+                    names[cls], (int)qok, q1, q2, (int)bok, pr.tin, bt2, o[0], o[1], o[2], d[0], d[1], d[2]);
+            return 1;
+          }
+        }
+      }
       tot[cls]++;
       if (prim >= 0) hits[cls]++;
       if (!res.cert) continue;
@@ -262,7 +306,8 @@ int main(int argc, char** argv) {
   }
   long all = 0, allc = 0;
   for (int k = 0; k < 7; k++) {
-    printf("%-18s rays %9ld  hits %9ld  certified %.5f\n", names[k], tot[k], hits[k], tot[k] ? (double)cert[k] / tot[k] : 0.0);
+    printf("%-18s rays %9ld  hits %9ld  pair certified %.5f  certified %.5f\n", names[k], tot[k], hits[k],
+           tot[k] ? (double)pcert[k] / tot[k] : 0.0, tot[k] ? (double)cert[k] / tot[k] : 0.0);
     all += tot[k];
     allc += cert[k];
   }

@@ -46,6 +46,7 @@ def test_scene_compile_facts():
     assert info.max_stack <= 24 and info.bvh_depth == 3
     vol = R.Scene(scene_path("cornell_box_volume")).info()
     assert vol.media == 2 and vol.n_materials == 6 and vol.n_textures == 3
+    assert vol.box_steps == 2  # both media's MakeBox boundaries take the box-level test (boxaa.h BoxAAPair)
     b1 = R.Scene(scene_path("final_render_book_1")).info()
     assert b1.legacy_schema == 1 and b1.spheres == 484 and b1.bvh_nodes == 511  # 484 leaves -> depth-9 tree
     b2 = R.Scene(scene_path("book2_final_scene_10000_samples")).info()
