@@ -1311,8 +1311,14 @@ __device__ __forceinline__ bool medium_t_lin(const void* recs, uint32_t moff, co
 #pragma unroll
       for (int j = 0; j < kBoxAAWords; j++) bw[j] = uf(bwr[j]);
       const BoxAAPairResult r = BoxAAPair<BoxMath>(bw, uf(bwr[6]), o.x, o.y, o.z, d.x, d.y, d.z, inv.x, inv.y, inv.z);
+      // stats counters (flushed by the counting kernels only; dead code elsewhere)
+      cnt.box++;
+      const bool lead = (int)__lane_id() == __builtin_amdgcn_readfirstlane((int)__lane_id());
+      cnt.box_wave += lead ? 1u : 0u;
+      cnt.box_wave_run += (lead && !__all(r.cert)) ? 1u : 0u;
       if (r.cert) {
         cert = true;
+        cnt.box_cert++;
         cnt.quad += 2u * kBoundaryAAMax;  // the two queries' face tests (the reference's count)
         // the second query's interval starts at fl(t1 + 0.0001): t1 itself for a large t1 (its face
         // then answers both queries), else past it (the exit face answers)

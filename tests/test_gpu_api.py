@@ -129,3 +129,37 @@ def test_kernel_time_is_gpu_busy_time_not_queue_time(have_gpu):
     assert 0 < st["sample_buffer_bytes"] <= (24 << 30)
     assert st["sample_buffer_bytes"] == 2 * 1000 * 256 * 256 * 12
     assert st["device_bytes_peak"] >= st["sample_buffer_bytes"] + 256 * 256 * 16
+
+
+@pytest.mark.parametrize("name,w,h,spp,frames", [("cornell_box_original", 64, 64, 1000, 6),
+                                                 ("cornell_box_volume", 64, 64, 1000, 6),
+                                                 ("book2_final_scene_10000_samples", 48, 48, 10000, 4)])
+def test_box_level_test_certifies_and_changes_no_bit(have_gpu, monkeypatch, name, w, h, spp, frames):
+    """The box-level test (boxaa.h; DESIGN.md §4 "Box-level test"): the compiler gives the scene's MakeBox
+    runs and MakeBox medium boundaries a box record, the counting kernel reports that it certifies
+    nearly every lane there (the rest run the six faces), and the accumulation equals, bit for bit, the
+    render with the test switched off (RT2_BOX_AA=0 at scene load: plain six-face runs)."""
+    def render(env):
+        if env is None:
+            monkeypatch.delenv("RT2_BOX_AA", raising=False)
+        else:
+            monkeypatch.setenv("RT2_BOX_AA", env)
+        sc = R.Scene(scene_path(name), R.DEFAULT_SEED)
+        tr = R.RayTracer(sc, 0)
+        tr.set_seed(R.DEFAULT_SEED)
+        tr.SetSamplesPerPixel(spp)
+        tr.OnResize((w, h))
+        tr.enable_stats(True)
+        tr.Render(frames)
+        acc = tr.Accumulation().copy()
+        st = tr.stats()
+        tr.close()
+        return sc.info().box_steps, acc, st
+    steps, acc, st = render(None)
+    steps0, acc0, st0 = render("0")
+    assert steps > 0 and steps0 == 0
+    assert st["box_tests"] > 0 and st0["box_tests"] == 0
+    assert st["box_certified"] >= 0.99 * st["box_tests"], (st["box_certified"], st["box_tests"])
+    assert st["box_wave_runs"] <= 0.01 * st["box_wave_visits"], (st["box_wave_runs"], st["box_wave_visits"])
+    assert st["rays"] == st0["rays"] and st["quad_tests"] == st0["quad_tests"]  # the reference's counts
+    assert np.array_equal(acc.view(np.uint32), acc0.view(np.uint32))

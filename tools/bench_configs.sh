@@ -25,6 +25,6 @@ run "C2 4-way, every rank" --steps 10 --warmup 2 --emulate-world 4 --emulate-ran
 run "C2 2-way, every rank" --steps 5 --warmup 2 --emulate-world 2 --emulate-rank all
 run "C3 book1 1920x1080 @ 500" $B1 --steps 2
 run "C4 cornell volume 1024^2 @ 4000" $VOL
-run "C4 8-way, every rank" $VOL --emulate-world 8 --emulate-rank all --warmup 0
+run "C4 8-way, every rank" $VOL --emulate-world 8 --emulate-rank all --warmup 1
 run "C5 book2 800^2 @ 10000" $B2 --warmup 0
-run "C5 8-way, every rank" $B2 --emulate-world 8 --emulate-rank all --warmup 0
+run "C5 8-way, every rank" $B2 --emulate-world 8 --emulate-rank all --warmup 1 --steps 2
