@@ -163,3 +163,30 @@ def test_box_level_test_certifies_and_changes_no_bit(have_gpu, monkeypatch, name
     assert st["box_wave_runs"] <= 0.01 * st["box_wave_visits"], (st["box_wave_runs"], st["box_wave_visits"])
     assert st["rays"] == st0["rays"] and st["quad_tests"] == st0["quad_tests"]  # the reference's counts
     assert np.array_equal(acc.view(np.uint32), acc0.view(np.uint32))
+
+
+def test_medium_box_far_away_matches_the_oracle(have_gpu):
+    """The medium's box-boundary test (boxaa.h BoxAAPair) at distances where the second boundary query
+    starts on the first hit itself: for t1 above 2^11, fl(t1 + 0.0001) = t1 (ConstantMedium.cpp:26-30), so
+    the entry face answers both queries and the medium has zero thickness there. The Cornell volume seen
+    from 6000 units away, bit-identical to the oracle (whose two queries run on the six faces)."""
+    from oracle.oracle import OracleScene
+    name, w, h, spp, frames = "cornell_box_volume", 24, 24, 4, 3
+    sc = R.Scene(scene_path(name), R.DEFAULT_SEED)
+    assert sc.info().box_steps == 2
+    cam = R.Camera((278.0, 278.0, -6000.0), (278.0, 278.0, 0.0), (0.0, 1.0, 0.0), 6.0, 0.0, 10.0)
+    tr = R.RayTracer(sc, 0)
+    tr.set_seed(R.DEFAULT_SEED)
+    tr.SetSamplesPerPixel(spp)
+    tr.OnResize((w, h))
+    tr.camera = cam
+    tr.enable_stats(True)
+    tr.Render(frames)
+    acc = tr.Accumulation()
+    st = tr.stats()
+    tr.close()
+    o = OracleScene(scene_path(name), R.DEFAULT_SEED)
+    o.set_camera(cam.center, cam.look_at, cam.view_up, cam.vfov, cam.defocus_angle, cam.focus_distance)
+    o_acc, _, _ = o.render(w, h, spp, frames, forward=True)
+    assert st["box_certified"] > 0
+    assert np.array_equal(acc.view(np.uint32), o_acc.view(np.uint32))
