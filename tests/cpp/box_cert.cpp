@@ -10,8 +10,10 @@
 // beside), grazing faces, starting on a face as a hit point rounded off the plane (leaving, re-entering,
 // along the face), starting inside, passing near the box, with zero direction components, intervals
 // ending exactly at a face's t and every tmax. Whenever the box test certifies a lane, its answer (face,
-// and the run's final kmax) must equal the run's: exits non-zero at the first disagreement. Prints the
-// counts and the certified fraction per ray class.
+// and the run's final kmax) must equal the run's, and whenever the medium form (BoxAAPair) certifies one,
+// its two boundary answers must equal the two ConstantMedium queries' over the six faces (render.hip
+// boundary_aa_pair): exits non-zero at the first disagreement. Prints the counts and the certified
+// fractions per ray class.
 #include <cfloat>
 #include <cmath>
 #include <cstdint>

@@ -82,11 +82,12 @@ def test_paired_program_steps_are_well_formed(tmp_path, scene, expect):
 
 
 def test_box_level_test_decides_as_the_six_face_run(tmp_path):
-    """boxaa.h BoxAATest (the kernel's kBoxAA step, host only): on random MakeBox boxes compiled by the
-    product, for rays entering through faces, edges and corners, grazing, leaving a face from a rounded
-    hit point, starting inside, passing near and with zero direction components, every lane the box test
-    certifies gets exactly the six-face run's answer (face and final interval key); the certified
-    fractions are printed (tests/cpp/box_cert.cpp)."""
+    """boxaa.h (the kernel's box-level tests, host only): on random MakeBox boxes compiled by the product,
+    for rays entering through faces, edges and corners, grazing, leaving a face from a rounded hit point,
+    starting inside, passing near and with zero direction components, every lane BoxAATest certifies gets
+    exactly the six-face run's answer (face and final interval key), and every lane BoxAAPair certifies
+    gets exactly the two ConstantMedium boundary queries' answers (t1, t2); the certified fractions are
+    printed (tests/cpp/box_cert.cpp)."""
     csrc = os.path.join(ROOT, "raytrace2_amd", "csrc")
     exe = str(tmp_path / "box_cert")
     r = subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
