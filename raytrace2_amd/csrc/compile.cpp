@@ -531,9 +531,11 @@ struct Flattener {
   // in its own space, MakeBox) also gets its children as consecutive QUADAA test words (8 words
   // each, rt2_layout.h), right after the medium's record, so that a kernel loads the whole boundary
   // at once with no child-ref indirection (two dependent scalar loads per quad and boundary query
-  // otherwise). Returns the medium record's word 3 (kBoundaryAAFlag | n << 24 | axis codes, 3 bits
-  // per child), or 0 (general path only). The general copy of the boundary is kept for kernels
-  // without the box path.
+  // otherwise). A MakeBox boundary (six faces, boxaa.h BoxAAWordsOf) also gets its box record after the
+  // quads' words and kBoundaryBoxFlag (the medium step's box-level test of both boundary queries,
+  // render.hip medium_t_lin). Returns the medium record's word 3 (kBoundaryAAFlag | kBoundaryBoxFlag |
+  // n << 24 | axis codes, 3 bits per child), or 0 (general path only). The general copy of the boundary
+  // is kept for kernels without the box path.
   uint32_t BoundaryAA(int i, uint32_t parent_xf, std::vector<float>& lind) {
     const Obj& o = s.objs[(size_t)i];
     if (o.kind != kList || o.children.empty() || o.children.size() > kBoundaryAAMax) return 0;

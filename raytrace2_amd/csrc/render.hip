@@ -1641,7 +1641,7 @@ __device__ __forceinline__ bool trace_linear(const RenderParams& P, const W& wra
       // a run of st.w quads with contiguous records, axis codes in st.y (3 bits each), tested in
       // order (issue-bound: one candidate at a time beats two interleaved, measured)
       const uint32_t run = st.w & kRunLenMask;
-      // A MakeBox run with a box record (aux bit 31; compile.cpp, for scenes with spheres): the box-level
+      // A MakeBox run with a box record (aux bit 31; compile.cpp, every scene unless RT2_BOX_AA=0): the box-level
       // test (boxaa.h) first. A certified lane takes the candidate face's answer and skips the run; the
       // wave runs the six faces only for the lanes it could not certify. The box record (six planes and
       // the margin constant, 2 records) lies right before the run's first face record; aux = run | flag

@@ -187,8 +187,8 @@ constexpr int kLinearMaxSteps = 1 << 16;
 #define RT2_LINEAR_MAX_RUN 10
 #endif
 constexpr uint32_t kLinearMaxRun = RT2_LINEAR_MAX_RUN;  // quads per run (3-bit axis codes + 1 bit in one word)
-// A quad step's aux word: the run length, and bit 31 for a MakeBox run whose box record (boxaa.h, 16 words:
-// the 12 box words, the margin constant, padding) lies right before the run's first face record
+// A quad step's aux word: the run length, and bit 31 for a MakeBox run whose box record (boxaa.h, 2 records:
+// the six planes, the margin constant, padding) lies right before the run's first face record
 constexpr uint32_t kRunLenMask = 0xFFu, kRunBoxFlag = 0x80000000u;
 static_assert(3 * kLinearMaxRun < 32, "a run's codes and their end bit fit one word");
 constexpr int kLinearMaxXformDepth = 8;  // deeper transform nesting uses the stack traversal
