@@ -122,7 +122,9 @@ bool BoxAAWordsOf(const float* const face[6], float out[6], float& mB) {
     if (code != 4u + (uint32_t)kAxis[j] || !RectAAWords(face[j], kAxis[j], tw[j])) return false;
   }
   // planes: lo / hi face index per axis (boxaa.h kBoxAAFaceMap: x- 3, x+ 1, y- 5, y+ 4, z- 2, z+ 0)
-  const int lo_face[3] = {3, 5, 2}, hi_face[3] = {1, 4, 0};
+  const int lo_face[3] = {(int)(kBoxAAFaceMap & 7u), (int)((kBoxAAFaceMap >> 6) & 7u), (int)((kBoxAAFaceMap >> 12) & 7u)};
+  const int hi_face[3] = {(int)((kBoxAAFaceMap >> 3) & 7u), (int)((kBoxAAFaceMap >> 9) & 7u),
+                          (int)((kBoxAAFaceMap >> 15) & 7u)};
   float plane[6];
   double B = 0;
   for (int k = 0; k < 3; k++) {
